@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Headline benchmark: PCM Msamples/s for 48 kHz -> 44.1 kHz polyphase
+resample + 8-track gain-ramped mixdown (BASELINE.json:2).
+
+Workload per GPU (weak scaling): 4096 input clips =
+512 mixes x 8 tracks, 10 s stereo fp32 @ 48 kHz (480000 frames) ->
+512 mixes x 441000 frames stereo fp32 @ 44.1 kHz.  Inputs are synthetic
+(splitmix64 PCM) generated directly in HBM by the
+library's xm_synth_pcm, outside the timed region.  One step = one
+xm_audio_mixer_process_strided call over the whole per-GPU batch (every
+track resampled, gained and summed; nothing cached between steps).
+
+Unit: 1 sample = one per-channel PCM sample of an input track;
+value = input samples of all ranks / wall time (max over ranks).
+
+Multi-GPU: one process per GPU (torchrun), mixes are independent, so each
+rank runs its own shard with no data-path collective; barrier + max-over-
+ranks timing only.
+
+Also reported (one JSON line on rank 0):
+  roofline     — algorithmic bytes per launch (inputs read once + output
+                 written once) / average kernel duration from HIP events on
+                 the stream the kernel runs on, vs the 8 TB/s HBM peak;
+                 traffic from the rocprofv3 PMC pass in profiles/ if present.
+  cpu_baseline — the C restatement (oracle/, "port") on a bounded sample of
+                 the same workload on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "xm-audio-utils_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+SEED = 0x584D4155
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+# 8 tracks: constant gains, fades, a crossfade pair, a step — every gain form
+# of the contract (include/xm_audio_common.h) is exercised every step.
+RAMPS = [
+    dict(gain0=0.9, gain1=0.9),
+    dict(gain0=0.0, gain1=0.8, ramp_start=0, ramp_len=44100),            # 1 s fade-in
+    dict(gain0=0.7, gain1=0.2, ramp_start=220500, ramp_len=88200),       # 2 s duck
+    dict(gain0=0.5, gain1=0.5),
+    dict(mode=1, ramp_start=132300, ramp_len=88200),                     # crossfade out
+    dict(gain0=0.0, gain1=1.0, ramp_start=132300, ramp_len=88200),       # crossfade in
+    dict(gain0=1.0, gain1=0.0, ramp_start=396900, ramp_len=44100),       # 1 s fade-out
+    dict(gain0=0.3, gain1=0.6, ramp_start=300000, ramp_len=0),           # step
+]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mixes", type=int, default=512, help="mixes per GPU (x8 tracks = clips)")
+    ap.add_argument("--tracks", type=int, default=8)
+    ap.add_argument("--frames", type=int, default=480000, help="input frames per track (10 s @ 48 kHz)")
+    ap.add_argument("--cpu-mixes", type=int, default=48, help="mixes in the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", action="store_true", help="bit-compare 2 mixes with the oracle after timing")
+    return ap.parse_args()
+
+
+def traffic_from_profiles():
+    """Latest corrected PMC traffic per launch (tools/profile_traffic.py output)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as fh:
+            d = json.load(fh)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, ramps):
+    import c_oracle as CO
+    import np_oracle as O
+    nmix = args.cpu_mixes
+    x = np.empty((nmix, args.tracks, args.frames, 2), np.float32)
+    for b in range(nmix):
+        for t in range(args.tracks):
+            x[b, t] = CO.gen_f32(SEED, b * args.tracks + t, 2, args.frames)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    _, used = CO.batch_resample_mix_f32(x, ramps, 147, 160, threads=threads)
+    dt = time.perf_counter() - t0
+    samples = x.size
+    del x
+    return {"value": round(samples / dt / 1e6, 2), "unit": "Msamples/s", "cores": int(used), "kind": "port",
+            "sample": f"{nmix} mixes x {args.tracks} tracks x {args.frames} frames x 2 ch fp32 "
+                      f"({samples / 1e6:.0f} M input samples, {dt:.2f} s wall), "
+                      f"oracle/xm_oracle.c -O3 -ffp-contract=off, OpenMP over mixes"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    import xmaudio as xm
+
+    B, ntr, N = args.mixes, args.tracks, args.frames
+    ramps = RAMPS[:ntr] if ntr <= len(RAMPS) else (RAMPS * ((ntr + 7) // 8))[:ntr]
+    mixer = xm.Mixer(48000, 44100, 2, "f32", mem="device", device=dev)
+    mixer.set_tracks(ramps)
+    F = mixer.out_frames(N)
+
+    x = torch.empty((B, ntr, N, 2), dtype=torch.float32, device="cuda")
+    y = torch.empty((B, F, 2), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    # clip ids are global: rank r owns clips [r*B*ntr, (r+1)*B*ntr)
+    xm.synth(x.data_ptr(), "f32", SEED, rank * B * ntr, B * ntr, 2, N, dev, stream.cuda_stream)
+    mixer.set_stream(stream.cuda_stream)
+    torch.cuda.synchronize()
+
+    def step():
+        mixer.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    launches_per_step = max(1, mixer.timing().n_launches)
+
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev0[i].record(stream)
+        step()
+        ev1[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in zip(ev0, ev1)]
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ok = None
+    if args.check and rank == 0:
+        import c_oracle as CO
+        xs = x[:2].cpu().numpy()
+        ref, _ = CO.batch_resample_mix_f32(xs, ramps, 147, 160, threads=os.cpu_count() or 1)
+        ok = bool(np.array_equal(y[:2].cpu().numpy().view(np.uint32), ref.view(np.uint32)))
+
+    in_samples = B * ntr * N * 2
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * in_samples / (elapsed / args.steps) / 1e6
+    alg_bytes = in_samples * 4 + B * F * 2 * 4
+    avg_launch_ms = float(np.mean(kern_ms)) / launches_per_step
+    achieved = alg_bytes / (avg_launch_ms * 1e-3) / 1e9
+    traffic = traffic_from_profiles()
+
+    if rank == 0:
+        cpu = None if args.no_cpu else cpu_baseline(args, ramps)
+        line = {
+            "metric": "PCM Msamples/sec (48k->44.1k resample + 8-track mix), batch 4096, 1/2/4/8 GPUs",
+            "value": round(value, 1), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "48k->44.1k polyphase resample (scipy resample_poly order) + 8-track "
+                                   "gain-ramp/crossfade mixdown, stereo fp32, 10 s clips",
+                       "clips_per_gpu": B * ntr, "mixes_per_gpu": B, "tracks": ntr, "frames_in": N,
+                       "frames_out": F, "channels": 2, "global_clips": world * B * ntr,
+                       "parallelism": f"dp{world} (independent mixes, no collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(avg_launch_ms, 4),
+                         "launches_per_step": launches_per_step},
+            "cpu_baseline": cpu,
+        }
+        if ok is not None:
+            line["parity_check_2mixes"] = ok
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

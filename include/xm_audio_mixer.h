@@ -1,0 +1,107 @@
+/*
+ * xm_audio_mixer.h — multi-track resample + gain-ramp + mixdown (C ABI).
+ *
+ * BUILD-OWNED ABI.  The reference snapshot has no headers
+ * (/root/reference/README.md:1 is the whole tree); BASELINE.json:5 names the
+ * prefix xm_audio_mixer_* and requires "host code stays in C and calls
+ * hand-written HIP kernels through a thin C-ABI shim".  These entry points
+ * are the ones SURVEY.md §8(b) proposes (create / set_tracks / process_batch /
+ * freep / strerror), plus a strided form and a stream hook for callers whose
+ * buffers already live in HBM.  Arithmetic: xm_audio_common.h.
+ *
+ * Data layout: each track / mix is interleaved PCM, frames x channels.
+ * One "mix" = n_tracks input tracks -> one output of out_frames frames.
+ *
+ * Threading: a handle is not re-entrant (one caller thread per handle);
+ * distinct handles may be used concurrently.  Calls are synchronous unless
+ * the caller installed a stream with xm_audio_mixer_set_stream(), in which
+ * case DEVICE-memory calls are stream-ordered and return without waiting
+ * (the cuBLAS/hipBLAS convention).
+ */
+#ifndef XM_AUDIO_MIXER_H
+#define XM_AUDIO_MIXER_H
+
+#include "xm_audio_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct XmAudioMixer XmAudioMixer;
+struct XmEffects;
+
+typedef struct XmMixerConfig {
+    int32_t in_rate;      /* Hz, every track (per-track rates: XmTrackDesc.in_rate) */
+    int32_t out_rate;     /* Hz of the mix */
+    int32_t channels;     /* 1 or 2 */
+    int32_t sample_fmt;   /* XmSampleFmt, input and output */
+    int32_t mem_kind;     /* XmMemKind of the in/out pointers */
+    int32_t device;       /* HIP device ordinal the handle runs on */
+    int32_t flags;        /* reserved, 0 */
+    int32_t reserved;
+} XmMixerConfig;
+
+typedef struct XmTrackDesc {
+    XmGainRamp gain;      /* per-track gain ramp / crossfade side */
+    int32_t    in_rate;   /* 0 = XmMixerConfig.in_rate; other values: XM_ENOSYS */
+    int32_t    reserved;
+} XmTrackDesc;
+
+/* Per-call timing of the last process call, from HIP events on the handle's
+ * stream (milliseconds; 0 where a stage did not run). */
+typedef struct XmMixerTiming {
+    float h2d_ms;         /* host->device staging (XM_MEM_HOST only) */
+    float kernel_ms;      /* all device compute of the call */
+    float d2h_ms;         /* device->host copy-back (XM_MEM_HOST only) */
+    int32_t n_launches;   /* kernels launched by the call */
+    int32_t reserved;
+} XmMixerTiming;
+
+/* Create a mixer.  Returns NULL on failure; *status (if non-NULL) gets the
+ * reason.  Fails with XM_EDEVICE when no GPU / HIP runtime is usable: there
+ * is no CPU fallback in the product library. */
+XM_API XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status);
+XM_API XmAudioMixer *xm_audio_mixer_create(const XmMixerConfig *cfg);
+
+/* Replace the track list (n_tracks in [1, 64]). */
+XM_API int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_tracks);
+
+/* Convenience: make track_from fade out and track_to fade in over
+ * [start, start+len) output frames (linear, g_from = 1 - g_to). */
+XM_API int xm_audio_mixer_set_crossfade(XmAudioMixer *m, int track_from, int track_to,
+                                 int64_t start, int64_t len);
+
+/* Attach an effects chain applied to every track after resampling and before
+ * the gain (NULL detaches).  The chain's rate/channels must match the mix. */
+XM_API int xm_audio_mixer_set_track_effects(XmAudioMixer *m, const struct XmEffects *fx);
+
+/* Output frames per mix for a given input length. */
+XM_API size_t xm_audio_mixer_out_frames(const XmAudioMixer *m, size_t frames_in);
+
+/* Install a caller-owned hipStream_t (NULL restores the handle's own stream). */
+XM_API int xm_audio_mixer_set_stream(XmAudioMixer *m, void *hip_stream);
+
+/* in  : batch*n_tracks pointers, mix-major: in[b*n_tracks + tr]
+ * out : batch pointers, each out_frames*channels samples
+ * All tracks hold frames_in frames.  Pointers of one call must all be of the
+ * configured XmMemKind. */
+XM_API int xm_audio_mixer_process_batch(XmAudioMixer *m, const void *const *in,
+                                 void *const *out, size_t batch, size_t frames_in);
+
+/* Same, for buffers laid out with constant strides (in SAMPLES, not bytes):
+ * track tr of mix b starts at in + b*in_mix_stride + tr*in_track_stride,
+ * mix b's output at out + b*out_mix_stride. */
+XM_API int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in,
+                                   ptrdiff_t in_track_stride, ptrdiff_t in_mix_stride,
+                                   void *out, ptrdiff_t out_mix_stride,
+                                   size_t batch, size_t frames_in);
+
+XM_API int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t);
+
+/* Destroy and NULL the handle (no-op on NULL). */
+XM_API void xm_audio_mixer_freep(XmAudioMixer **m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XM_AUDIO_MIXER_H */

@@ -1,0 +1,72 @@
+/*
+ * xm_effects.h — biquad / FIR effects chain over batches of clips (C ABI).
+ *
+ * BUILD-OWNED ABI (reference has no headers: /root/reference/README.md:1;
+ * prefix xm_effects_* from BASELINE.json:5, signatures from SURVEY.md §8(b)).
+ *
+ * Arithmetic (pinned to scipy 1.15.3 float32):
+ *  biquad section (b0,b1,b2,1,a1,a2), transposed direct form II, state zero at
+ *  clip start, per channel, sections applied in insertion order:
+ *      y  = b0*x + z0;  z0 = (b1*x - a1*y) + z1;  z1 = b2*x - a2*y;  x = y
+ *  (scipy sosfilt, _signaltools.py:4601 / _sosfilt.pyx)
+ *  FIR of K taps, causal, output length = input length:
+ *      acc=+0; for t=0..K-1: acc = acc + x[n-K+1+t]*h[K-1-t]   (x<0 := 0)
+ *  (scipy upfirdn(h, x)[:N], _upfirdn.py:107)
+ *  Effects run in insertion order; consecutive biquads form one cascade.
+ */
+#ifndef XM_EFFECTS_H
+#define XM_EFFECTS_H
+
+#include "xm_audio_common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct XmEffects XmEffects;
+
+typedef enum XmEqBand {
+    XM_EQ_PEAKING   = 0,
+    XM_EQ_LOWSHELF  = 1,
+    XM_EQ_HIGHSHELF = 2,
+    XM_EQ_LOWPASS   = 3,
+    XM_EQ_HIGHPASS  = 4
+} XmEqBand;
+
+typedef struct XmEffectsConfig {
+    int32_t rate;        /* Hz */
+    int32_t channels;    /* 1 or 2 */
+    int32_t mem_kind;    /* XmMemKind of in/out pointers */
+    int32_t device;      /* HIP device ordinal */
+} XmEffectsConfig;
+
+XM_API XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status);
+/* Host-memory chain on device 0 (SURVEY.md §8(b) form; n_devices must be 1). */
+XM_API XmEffects *xm_effects_create(int rate, int channels, int n_devices);
+
+/* sos = {b0, b1, b2, a0, a1, a2}; a0 must be 1 (as scipy sosfilt requires). */
+XM_API int xm_effects_add_biquad(XmEffects *e, const float sos[6]);
+
+/* RBJ audio-EQ-cookbook section designed in fp64 and cast to fp32.
+ * q is Q (peaking / pass filters) or shelf slope S (shelves). */
+XM_API int xm_effects_add_eq_band(XmEffects *e, int band, double f0_hz, double gain_db, double q);
+
+/* FIR with K taps (1 <= K <= 4096), copied. */
+XM_API int xm_effects_add_fir(XmEffects *e, const float *h, int K);
+
+/* Number of effects and the coefficients of biquad i (for inspection). */
+XM_API int xm_effects_count(const XmEffects *e);
+XM_API int xm_effects_get_biquad(const XmEffects *e, int index, float sos[6]);
+
+XM_API int xm_effects_set_stream(XmEffects *e, void *hip_stream);
+
+/* in/out: batch pointers of frames*channels float32 samples (in == out allowed). */
+XM_API int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const *out,
+                             size_t batch, size_t frames);
+
+XM_API void xm_effects_freep(XmEffects **e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XM_EFFECTS_H */

@@ -1,0 +1,288 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar (BASELINE.json:5): bit-exact for s16 mix/gain and — stricter than the
+north_star's ±1 ULP float32 allowance — bit-exact for fp32 resample / mix /
+biquad / FIR, since the kernels keep scipy's separately-rounded order.
+Small cases compare with the committed scipy golden vectors; larger ones
+with the C restatement (oracle/xm_oracle.c), itself pinned to those vectors
+by tests/test_oracle.py.
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, golden, manifest, ulp_diff
+
+import c_oracle as CO
+import np_oracle as O
+
+pytestmark = pytest.mark.gpu
+SEED = O.SEED
+
+
+def _resample_cases():
+    z = golden("resample.npz")
+    return sorted(k[:-6] for k in z.files if k.endswith("__meta"))
+
+
+@pytest.mark.parametrize("name", _resample_cases())
+def test_resample_f32_golden(xm, gpu, name):
+    z = golden("resample.npz")
+    fi, fo, N, Cc, clip = (int(v) for v in z[f"{name}__meta"])
+    x = O.gen_f32(SEED, clip, Cc, N)
+    m = xm.Mixer(fi, fo, Cc, "f32")
+    y = m.process(x[None, None])[0]
+    ref = z[f"{name}__y"].reshape(y.shape)
+    assert bits_equal(y, ref), f"max ulp {ulp_diff(y, ref)}"
+
+
+@pytest.mark.parametrize("kind", ["silence", "fullscale", "denormal", "impulse"])
+def test_resample_f32_special(xm, gpu, kind):
+    z = golden("resample.npz")
+    x, ref = z[f"special_{kind}__x"], z[f"special_{kind}__y"]
+    y = xm.Mixer(48000, 44100, 2, "f32").process(x[None, None])[0]
+    assert bits_equal(y, ref)
+
+
+def test_resample_s16_saturating(xm, gpu):
+    z = golden("resample_s16.npz")
+    y = xm.Mixer(48000, 44100, 2, "s16").process(z["x"][None, None])[0]
+    assert bits_equal(y, z["y"])
+
+
+def test_config1_s16_44k_to_48k_full_clip(xm, gpu):
+    """BASELINE.json:7: single mono 44.1k->48k s16, 10 s — GPU equals the CPU path."""
+    x = O.gen_s16(SEED, 0, 1, 441000)
+    y = xm.Mixer(44100, 48000, 1, "s16").process(x[None, None])[0]
+    assert y.shape == (480000, 1)
+    assert hashlib.sha256(y.tobytes()).hexdigest() == manifest()["config1_sha256"]
+
+
+def test_mix_s16_8track_golden(xm, gpu):
+    """Config 3 shape: 8-track s16 mix with ramps, crossfade and saturation."""
+    z = golden("mix.npz")
+    ramps = json.loads(str(z["s16_mix8__ramps"]))
+    tr = [O.gen_s16(SEED, 200 + t, 2, 4800) for t in range(8)]
+    tr[0][10:20] = 32767
+    tr[1][10:20] = 32767
+    tr[2][30:40] = -32768
+    m = xm.Mixer(48000, 48000, 2, "s16")
+    m.set_tracks(ramps)
+    y = m.process(np.stack(tr)[None])[0]
+    assert bits_equal(y, z["s16_mix8__y"])
+
+
+def test_resample_mix_s16_golden(xm, gpu):
+    z = golden("mix.npz")
+    ramps = json.loads(str(z["s16_mix8__ramps"]))[:4]
+    tr = [O.gen_s16(SEED, 200 + t, 2, 4800) for t in range(4)]
+    tr[0][10:20] = 32767
+    tr[1][10:20] = 32767
+    tr[2][30:40] = -32768
+    m = xm.Mixer(48000, 44100, 2, "s16")
+    m.set_tracks(ramps)
+    assert bits_equal(m.process(np.stack(tr)[None])[0], z["s16_resample4__y"])
+
+
+def test_resample_mix_f32_golden(xm, gpu):
+    """Headline op at fixture size: resample 48k->44.1k + 8-track ramped mix."""
+    z = golden("mix.npz")
+    ramps = json.loads(str(z["f32_resample8__ramps"]))
+    xs = np.stack([O.gen_f32(SEED, 100 + t, 2, 4800) for t in range(8)])
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(ramps)
+    y = m.process(xs[None])[0]
+    assert bits_equal(y, z["f32_resample8__y"]), f"max ulp {ulp_diff(y, z['f32_resample8__y'])}"
+
+
+HEADLINE_RAMPS = [
+    dict(gain0=0.9), dict(gain0=0.0, gain1=0.8, ramp_start=1000, ramp_len=30000),
+    dict(gain0=0.7, gain1=0.2, ramp_start=20000, ramp_len=4410), dict(gain0=0.5),
+    dict(mode=1, ramp_start=30000, ramp_len=8000), dict(gain0=0.0, gain1=1.0, ramp_start=30000, ramp_len=8000),
+    dict(gain0=1.25, gain1=0.75, ramp_start=0, ramp_len=44100), dict(gain0=0.3, gain1=0.6, ramp_start=40000),
+]
+
+
+@pytest.mark.parametrize("frames", [48000, 48000 + 77])
+def test_resample_mix_f32_vs_c_oracle_batch(xm, gpu, frames):
+    """4 mixes x 8 tracks x ~1 s stereo, every output bit-compared with the C oracle."""
+    B, ntr = 4, 8
+    x = np.stack([np.stack([O.gen_f32(SEED, 1000 + 8 * b + t, 2, frames) for t in range(ntr)]) for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(HEADLINE_RAMPS)
+    y = m.process(x)
+    ref, _ = CO.batch_resample_mix_f32(x, HEADLINE_RAMPS, 147, 160, threads=8)
+    assert bits_equal(y, ref), f"max ulp {ulp_diff(y, ref)}"
+
+
+def test_resample_44_to_48_mix_vs_c_oracle(xm, gpu):
+    x = np.stack([O.gen_f32(SEED, 500 + t, 2, 44100) for t in range(3)])[None]
+    ramps = HEADLINE_RAMPS[:3]
+    m = xm.Mixer(44100, 48000, 2, "f32")
+    m.set_tracks(ramps)
+    y = m.process(x)[0]
+    assert bits_equal(y, CO.resample_mix_f32(list(x[0]), ramps, 160, 147))
+
+
+def test_mono_and_identity_ratio(xm, gpu):
+    x = np.stack([O.gen_f32(SEED, 600 + t, 1, 3000) for t in range(5)])[None]
+    ramps = HEADLINE_RAMPS[:5]
+    m = xm.Mixer(48000, 44100, 1, "f32")
+    m.set_tracks(ramps)
+    assert bits_equal(m.process(x)[0], CO.resample_mix_f32(list(x[0]), ramps, 147, 160))
+    m2 = xm.Mixer(48000, 48000, 1, "f32")
+    m2.set_tracks(ramps)
+    assert bits_equal(m2.process(x)[0], CO.mix_f32(list(x[0]), ramps))
+
+
+def test_large_s16_mix_vs_c_oracle(xm, gpu):
+    """Config 3 arithmetic on 16 mixes x 8 tracks x 2 s stereo."""
+    B, ntr, F = 16, 8, 96000
+    x = np.stack([np.stack([O.gen_s16(SEED, 3000 + 8 * b + t, 2, F) for t in range(ntr)]) for b in range(B)])
+    ramps = [dict(gain0_q15=q, gain1_q15=q2, ramp_start=s, ramp_len=ln, mode=md)
+             for q, q2, s, ln, md in [(32768, 32768, 0, 0, 0), (0, 32768, 100, 20000, 0), (65535, 100, 0, 96000, 0),
+                                      (16384, 16384, 0, 0, 0), (0, 0, 50000, 9000, 1), (0, 32768, 50000, 9000, 0),
+                                      (40000, 3, 70000, 13, 0), (7, 60000, 48000, 0, 0)]]
+    m = xm.Mixer(48000, 48000, 2, "s16")
+    m.set_tracks(ramps)
+    y = m.process(x)
+    ref, _ = CO.batch_mix_s16(x, ramps, threads=8)
+    assert bits_equal(y, ref)
+
+
+def test_crossfade_helper(xm, gpu):
+    x = np.stack([O.gen_f32(SEED, 700 + t, 2, 4800) for t in range(2)])[None]
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks([dict(gain0=1.0), dict(gain0=1.0)])
+    m.set_crossfade(0, 1, 1000, 2000)
+    ramps = [dict(mode=1, ramp_start=1000, ramp_len=2000), dict(gain0=0.0, gain1=1.0, ramp_start=1000, ramp_len=2000)]
+    assert bits_equal(m.process(x)[0], CO.resample_mix_f32(list(x[0]), ramps, 147, 160))
+
+
+def test_ragged_lengths(xm, gpu):
+    for N in (1, 2, 22, 23, 159, 160, 161, 321, 1001):
+        x = np.stack([O.gen_f32(SEED, 800 + t, 2, N) for t in range(3)])[None]
+        m = xm.Mixer(48000, 44100, 2, "f32")
+        m.set_tracks(HEADLINE_RAMPS[:3])
+        y = m.process(x)[0]
+        assert bits_equal(y, CO.resample_mix_f32(list(x[0]), HEADLINE_RAMPS[:3], 147, 160)), N
+
+
+def test_empty_inputs(xm, gpu):
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    y = m.process(np.zeros((1, 1, 0, 2), np.float32))
+    assert y.shape == (1, 0, 2)
+    y = m.process(np.zeros((0, 1, 100, 2), np.float32))
+    assert y.shape == (0, 92, 2)
+
+
+def test_effects_biquad_fir_golden(xm, gpu):
+    z = golden("effects.npz")
+    e = xm.Effects(48000, 2)
+    for b in z["bands"]:
+        e.add_eq_band(int(b[0]), float(b[2]), float(b[3]), float(b[4]))
+    for i in range(5):
+        assert bits_equal(e.biquad(i), z["sos"][i])
+    assert bits_equal(e.process(z["x"][None])[0], z["y_biquad"])
+    f = xm.Effects(48000, 2)
+    f.add_fir(z["h63"])
+    assert bits_equal(f.process(z["x"][None])[0], z["y_fir63"])
+    assert bits_equal(f.process(z["x"][None].copy(), inplace=True)[0], z["y_fir63"])
+    g = xm.Effects(48000, 1)
+    g.add_fir(z["h7"])
+    assert bits_equal(g.process(z["x"][None, :1000, :1])[0, :, 0], z["y_fir7_mono"])
+
+
+def test_effects_chain_vs_c_oracle(xm, gpu):
+    z = golden("effects.npz")
+    x = np.stack([O.gen_f32(SEED, 900 + b, 2, 20000) for b in range(6)])
+    e = xm.Effects(48000, 2)
+    for s in z["sos"][:3]:
+        e.add_biquad(s)
+    e.add_fir(z["h63"])
+    for s in z["sos"][3:]:
+        e.add_biquad(s)
+    y = e.process(x)
+    for b in range(6):
+        r = CO.biquad_f32(CO.fir_f32(CO.biquad_f32(x[b], z["sos"][:3]), z["h63"]), z["sos"][3:])
+        assert bits_equal(y[b], r), b
+
+
+def test_mixer_with_track_eq_vs_c_oracle(xm, gpu):
+    """Config 4 chain: resample -> 5-band EQ -> gain -> ordered mix."""
+    z = golden("effects.npz")
+    x = np.stack([O.gen_f32(SEED, 950 + t, 2, 9600) for t in range(4)])[None]
+    ramps = HEADLINE_RAMPS[:4]
+    e = xm.Effects(44100, 2)
+    for s in z["sos"]:
+        e.add_biquad(s)
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(ramps)
+    m.set_track_effects(e)
+    y = m.process(x)[0]
+    r = [CO.biquad_f32(CO.resample_f32(t, 147, 160), z["sos"]) for t in x[0]]
+    assert bits_equal(y, CO.mix_f32(r, ramps))
+
+
+def test_device_memory_strided_and_ptrs(xm, gpu):
+    """XM_MEM_DEVICE through torch-allocated HBM: strided, pointer tables and a
+    caller stream all give the host-mode bits."""
+    import torch
+    B, ntr, N = 3, 8, 9600
+    x = np.stack([np.stack([O.gen_f32(SEED, 1200 + 8 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    host = xm.Mixer(48000, 44100, 2, "f32")
+    host.set_tracks(HEADLINE_RAMPS)
+    ref = host.process(x)
+    dev = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    dev.set_tracks(HEADLINE_RAMPS)
+    F = dev.out_frames(N)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.zeros((B, F, 2), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    dev.process_strided(xd.data_ptr(), N * 2, ntr * N * 2, yd.data_ptr(), F * 2, B, N)
+    assert bits_equal(yd.cpu().numpy(), ref)
+    # permuted pointer table (non-strided)
+    perm = [2, 0, 1]
+    yd2 = torch.zeros_like(yd)
+    ins = [xd[b, t].data_ptr() for b in perm for t in range(ntr)]
+    outs = [yd2[i].data_ptr() for i in range(B)]
+    dev.process_ptrs(ins, outs, B, N)
+    assert bits_equal(yd2.cpu().numpy(), ref[perm])
+    # caller stream: stream-ordered, asynchronous
+    s = torch.cuda.Stream()
+    yd3 = torch.zeros_like(yd)
+    dev.set_stream(s.cuda_stream)
+    dev.process_strided(xd.data_ptr(), N * 2, ntr * N * 2, yd3.data_ptr(), F * 2, B, N)
+    s.synchronize()
+    dev.set_stream(None)
+    assert bits_equal(yd3.cpu().numpy(), ref)
+
+
+def test_synth_matches_oracle_generator(xm, gpu):
+    import torch
+    t = torch.empty((3, 1000, 2), dtype=torch.float32, device="cuda")
+    xm.synth(t.data_ptr(), "f32", SEED, 4094, 3, 2, 1000)
+    for c in range(3):
+        assert bits_equal(t[c].cpu().numpy(), O.gen_f32(SEED, 4094 + c, 2, 1000))
+    s = torch.empty((2, 777, 1), dtype=torch.int16, device="cuda")
+    xm.synth(s.data_ptr(), "s16", SEED, 5, 2, 1, 777)
+    assert bits_equal(s[0].cpu().numpy(), O.gen_s16(SEED, 5, 1, 777))
+
+
+def test_errors(xm, gpu):
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    with pytest.raises(xm.XmError) as e:
+        m.set_tracks([dict(gain0_q15=70000)])
+    assert e.value.code == xm.XM_EINVAL
+    with pytest.raises(xm.XmError):
+        m.set_tracks([dict()] * 65)
+    with pytest.raises(xm.XmError) as e:
+        m.set_tracks([dict(in_rate=22050)])
+    assert e.value.code == xm.XM_ENOSYS
+    with pytest.raises(xm.XmError):
+        xm.Mixer(48000, 44100, 2, "f32", device=99)
+    e2 = xm.Effects(48000, 2)
+    with pytest.raises(xm.XmError):
+        e2.add_biquad([1, 0, 0, 2, 0, 0])   # a0 != 1

@@ -1,0 +1,257 @@
+// xm_mix_generic.hip — generic gfx950 kernels for any rate pair / channel
+// count / track count: LDS-staged polyphase resample + gain + ordered mix, and
+// the no-resample integer (s16 Q15) and fp32 mixes.
+//
+// Arithmetic: include/xm_audio_common.h (pinned to scipy 1.15.3 resample_poly,
+// SURVEY.md §8(a) a2/a3/a6/a7).  The headline 48k->44.1k stereo fp32 path has
+// its own kernel (xm_resample_fast.hip); this file is the reference-order
+// fallback every other configuration uses, and the s16 mixer (config 3).
+#include "xm_device.h"
+
+namespace {
+
+constexpr int GEN_THREADS = 256;
+constexpr int GEN_OPT = 4;                          // outputs per thread per block
+constexpr int GEN_CHUNK = GEN_THREADS * GEN_OPT;    // output frames per block
+
+// Block = (output chunk, mix).  For every track: stage the input frames the
+// chunk needs into LDS (zero outside [0, N) — equivalent to scipy's skip, see
+// DESIGN.md "zero padding"), then each thread forms its outputs tap by tap in
+// ascending order (oldest input first) exactly as upfirdn does.
+template <int C, bool S16>
+__global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob j)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int L = j.rs.L, M = j.rs.M, T = j.rs.T, rm = j.rs.rm;
+    const int b = blockIdx.y;
+    const int64_t m0 = (int64_t)blockIdx.x * GEN_CHUNK;
+    const int64_t m1 = min(m0 + GEN_CHUNK, (int64_t)j.frames_out);
+    const int64_t N = j.frames_in;
+
+    float *H = lds;                                  // L*T
+    float *tile = lds + ((L * T + 3) & ~3);          // span*C
+    for (int i = threadIdx.x; i < L * T; i += GEN_THREADS) H[i] = j.rs.H[i];
+
+    const int64_t jlo = ((m0 + rm) * M) / L - T + 1;
+    const int64_t jhi = ((m1 - 1 + rm) * M) / L;     // inclusive
+    const int span = (int)(jhi - jlo + 1);
+
+    float accf[GEN_OPT][C];
+    int32_t acci[GEN_OPT][C];
+#pragma unroll
+    for (int o = 0; o < GEN_OPT; ++o)
+#pragma unroll
+        for (int c = 0; c < C; ++c) { accf[o][c] = 0.0f; acci[o][c] = 0; }
+
+    for (int tr = 0; tr < j.n_tracks; ++tr) {
+        __syncthreads();
+        if (S16) {
+            const int16_t *x = (const int16_t *)xm_track_ptr(j, b, tr, 2);
+            for (int i = threadIdx.x; i < span * C; i += GEN_THREADS) {
+                int64_t f = jlo + i / C;
+                tile[i] = (f >= 0 && f < N) ? (float)x[f * C + i % C] : 0.0f;
+            }
+        } else {
+            const float *x = (const float *)xm_track_ptr(j, b, tr, 4);
+            for (int i = threadIdx.x; i < span * C; i += GEN_THREADS) {
+                int64_t f = jlo + i / C;
+                tile[i] = (f >= 0 && f < N) ? x[f * C + i % C] : 0.0f;
+            }
+        }
+        __syncthreads();
+        const XmhGain g = j.gains[tr];
+#pragma unroll
+        for (int o = 0; o < GEN_OPT; ++o) {
+            const int64_t m = m0 + threadIdx.x + o * GEN_THREADS;
+            if (m >= m1) continue;
+            const int64_t Mx = (m + rm) * M;
+            const int ph = (int)(Mx % L);
+            const int jb = (int)(Mx / L - T + 1 - jlo);
+            const float *h = H + ph * T;
+            const float *xt = tile + jb * C;
+            float r[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) r[c] = 0.0f;
+            for (int t = 0; t < T; ++t) {
+                const float hv = h[t];
+#pragma unroll
+                for (int c = 0; c < C; ++c) r[c] = r[c] + xt[t * C + c] * hv;
+            }
+            if (S16) {
+                const int32_t gq = xm_gain_q15(g, m);
+#pragma unroll
+                for (int c = 0; c < C; ++c) acci[o][c] += xm_q15_term(xm_round_sat16(r[c]), gq);
+            } else {
+                const float gf = xm_gain_f32(g, m);
+#pragma unroll
+                for (int c = 0; c < C; ++c) accf[o][c] = accf[o][c] + gf * r[c];
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < GEN_OPT; ++o) {
+        const int64_t m = m0 + threadIdx.x + o * GEN_THREADS;
+        if (m >= m1) continue;
+        if (S16) {
+            int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[m * C + c] = xm_sat16(acci[o][c]);
+        } else {
+            float *y = (float *)xm_out_ptr(j, b, 4);
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[m * C + c] = accf[o][c] + 0.0f;  // -0 -> +0 (scipy acc starts at +0)
+        }
+    }
+}
+
+// ---- no-resample mixes (L == M) -------------------------------------------
+// s16 Q15 mix (config 3): each thread owns 8 consecutive samples (16 B) of the
+// mix output and reads the same 16 B from every track: fully coalesced
+// dwordx4 streams, int32 accumulate, saturate once.  Gains are evaluated per
+// frame; the fast path (gain constant across the thread's frames) evaluates
+// them once.
+constexpr int MIX_THREADS = 256;
+
+template <int C>
+__global__ __launch_bounds__(MIX_THREADS) void k_mix_s16(XmhMixJob j)
+{
+    constexpr int SPT = 8;                 // samples per thread (16 B)
+    constexpr int FPT = SPT / C;           // frames per thread
+    const int b = blockIdx.y;
+    const int64_t total = j.frames_out * C;
+    const int64_t s0 = ((int64_t)blockIdx.x * MIX_THREADS + threadIdx.x) * SPT;
+    if (s0 >= total) return;
+    const int64_t f0 = s0 / C;
+    const bool full = s0 + SPT <= total;
+
+    int32_t acc[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) acc[i] = 0;
+
+    for (int tr = 0; tr < j.n_tracks; ++tr) {
+        const int16_t *x = (const int16_t *)xm_track_ptr(j, b, tr, 2) + s0;
+        int16_t v[SPT];
+        if (full && ((((uintptr_t)x) & 15) == 0)) {
+            const int4 q = *(const int4 *)x;
+            __builtin_memcpy(v, &q, 16);
+        } else {
+#pragma unroll
+            for (int i = 0; i < SPT; ++i) v[i] = (s0 + i < total) ? x[i] : 0;
+        }
+        const XmhGain g = j.gains[tr];
+        if (xm_gain_const(g, f0, f0 + FPT - 1)) {
+            const int32_t gq = xm_gain_q15(g, f0);
+#pragma unroll
+            for (int i = 0; i < SPT; ++i) acc[i] += xm_q15_term(v[i], gq);
+        } else {
+#pragma unroll
+            for (int f = 0; f < FPT; ++f) {
+                const int32_t gq = xm_gain_q15(g, f0 + f);
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc[f * C + c] += xm_q15_term(v[f * C + c], gq);
+            }
+        }
+    }
+    int16_t o[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) o[i] = xm_sat16(acc[i]);
+    int16_t *y = (int16_t *)xm_out_ptr(j, b, 2) + s0;
+    if (full && ((((uintptr_t)y) & 15) == 0)) {
+        int4 q;
+        __builtin_memcpy(&q, o, 16);
+        *(int4 *)y = q;
+    } else {
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) y[i] = o[i];
+    }
+}
+
+// fp32 mix without resampling: acc = +0; acc = acc + g*x in track order.
+template <int C>
+__global__ __launch_bounds__(MIX_THREADS) void k_mix_f32(XmhMixJob j)
+{
+    constexpr int SPT = 4;                 // 16 B per thread
+    constexpr int FPT = SPT / C;
+    const int b = blockIdx.y;
+    const int64_t total = j.frames_out * C;
+    const int64_t s0 = ((int64_t)blockIdx.x * MIX_THREADS + threadIdx.x) * SPT;
+    if (s0 >= total) return;
+    const int64_t f0 = s0 / C;
+    const bool full = s0 + SPT <= total;
+    float acc[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) acc[i] = 0.0f;
+    for (int tr = 0; tr < j.n_tracks; ++tr) {
+        const float *x = (const float *)xm_track_ptr(j, b, tr, 4) + s0;
+        float v[SPT];
+        if (full && ((((uintptr_t)x) & 15) == 0)) {
+            const float4 q = *(const float4 *)x;
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < SPT; ++i) v[i] = (s0 + i < total) ? x[i] : 0.0f;
+        }
+        const XmhGain g = j.gains[tr];
+#pragma unroll
+        for (int f = 0; f < FPT; ++f) {
+            const float gf = xm_gain_f32(g, f0 + f);
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[f * C + c] = acc[f * C + c] + gf * v[f * C + c];
+        }
+    }
+    float *y = (float *)xm_out_ptr(j, b, 4) + s0;
+    if (full && ((((uintptr_t)y) & 15) == 0)) {
+        *(float4 *)y = float4{acc[0] + 0.0f, acc[1] + 0.0f, acc[2] + 0.0f, acc[3] + 0.0f};
+    } else {
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) y[i] = acc[i] + 0.0f;
+    }
+}
+
+template <typename K>
+int launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const XmhMixJob &j)
+{
+    if (grid.x == 0 || grid.y == 0) return 0;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return -1001;
+    hipLaunchKernelGGL(kern, grid, block, lds, s, j);
+    return hipGetLastError() == hipSuccess ? 0 : -1001;
+}
+
+}  // namespace
+
+// Generic launcher (called by xmh_launch_mix in xm_shim.hip when the fast
+// kernel does not apply).
+extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_launches)
+{
+    hipStream_t s = (hipStream_t)stream;
+    const int C = j->channels;
+    const bool s16 = j->fmt == 1;
+    if (j->frames_out == 0 || j->n_mix == 0) return 0;
+    if (j->rs.L == j->rs.M) {
+        const int spt = s16 ? 8 : 4;
+        const int64_t samples = j->frames_out * C;
+        dim3 grid((unsigned)((samples + (int64_t)MIX_THREADS * spt - 1) / ((int64_t)MIX_THREADS * spt)),
+                  (unsigned)j->n_mix);
+        int rc;
+        if (s16) rc = C == 1 ? launch(k_mix_s16<1>, grid, MIX_THREADS, 0, s, *j)
+                             : launch(k_mix_s16<2>, grid, MIX_THREADS, 0, s, *j);
+        else     rc = C == 1 ? launch(k_mix_f32<1>, grid, MIX_THREADS, 0, s, *j)
+                             : launch(k_mix_f32<2>, grid, MIX_THREADS, 0, s, *j);
+        if (n_launches) *n_launches += 1;
+        return rc;
+    }
+    const int64_t L = j->rs.L, M = j->rs.M, T = j->rs.T;
+    const int64_t span = (GEN_CHUNK * M) / L + 2 + T;
+    const size_t lds = (size_t)(((L * T + 3) & ~3) + span * C) * sizeof(float);
+    if (lds > 160 * 1024) return -1003;  // XM_ENOSYS: ratio too extreme for the LDS-staged path
+    dim3 grid((unsigned)((j->frames_out + GEN_CHUNK - 1) / GEN_CHUNK), (unsigned)j->n_mix);
+    int rc;
+    if (s16) rc = C == 1 ? launch(k_resample_mix_generic<1, true>, grid, GEN_THREADS, lds, s, *j)
+                         : launch(k_resample_mix_generic<2, true>, grid, GEN_THREADS, lds, s, *j);
+    else     rc = C == 1 ? launch(k_resample_mix_generic<1, false>, grid, GEN_THREADS, lds, s, *j)
+                         : launch(k_resample_mix_generic<2, false>, grid, GEN_THREADS, lds, s, *j);
+    if (n_launches) *n_launches += 1;
+    return rc;
+}

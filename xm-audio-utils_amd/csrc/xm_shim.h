@@ -1,0 +1,115 @@
+/*
+ * xm_shim.h — internal C ABI between the C host layer (src/ C files) and the HIP
+ * side (csrc/ .hip files).  Plain C types only; every hipError_t is mapped to an
+ * XM_* status inside the shim (SURVEY.md §8(b) "Shim exports").
+ *
+ * Nothing here is public: callers use include/xm_audio_mixer.h and
+ * include/xm_effects.h.
+ */
+#ifndef XM_SHIM_H
+#define XM_SHIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------- device gain descriptor (32 B, one per track) ------------------
+ * F32: g = g0 + step * (float)k          (step precomputed on the host in fp32)
+ * Q15: g = q0 + (qd * k) / len           (int64, C truncation)
+ * k = clamp(n - start, 0, len); len == 0 => g = n >= start ? end : begin.
+ * flags bit0: crossfade-out (g := 1 - g, Q15: 32768 - g). */
+typedef struct XmhGain {
+    float   g0, g1, step;     /* F32 ramp (xfade-out: g0=0, g1=1) */
+    int32_t q0, q1;           /* Q15 ramp (xfade-out: 0, 32768) */
+    int32_t len;              /* ramp length, < 2^24 */
+    int32_t flags;            /* XMH_GAIN_* */
+    int32_t pad;
+    int64_t start;            /* ramp start (output frame) */
+} XmhGain;                    /* 40 B */
+#define XMH_GAIN_XFADE_OUT 1u
+
+/* ---------- resampler table on the device -------------------------------- */
+typedef struct XmhResample {
+    int32_t L, M, T, rm;      /* L == M == 1: no resampling */
+    const float *H;           /* device, L*T floats (phase-major) */
+    const float *Hrun;        /* device, run-ordered table for the fast path (or NULL) */
+} XmhResample;
+
+/* ---------- one mix job (all pointers device) ------------------------------
+ * Track tr of mix b: in_ptrs ? in_ptrs[b*n_tracks+tr]
+ *                            : in + (b*in_mix_stride + tr*in_track_stride) samples.
+ * Output of mix b : out_ptrs ? out_ptrs[b] : out + b*out_mix_stride samples. */
+typedef struct XmhMixJob {
+    int32_t fmt;              /* 1 = s16, 2 = f32 */
+    int32_t channels;         /* 1 or 2 */
+    int32_t n_tracks;         /* 1..64 */
+    int32_t n_mix;
+    int64_t frames_in, frames_out;
+    const void *in;
+    int64_t in_track_stride, in_mix_stride;
+    const void *const *in_ptrs;
+    void *out;
+    int64_t out_mix_stride;
+    void *const *out_ptrs;
+    const XmhGain *gains;     /* device, n_tracks entries */
+    int32_t unity;            /* 1: every gain is constant 1.0 (pure resample fast path) */
+    int32_t reserved;
+    XmhResample rs;
+    /* optional per-track effects chain (config 4): device sos table */
+    const float *sos;         /* n_sos x 6, or NULL */
+    int32_t n_sos;
+    int32_t reserved2;
+    void *scratch;            /* device scratch for staged paths */
+    size_t scratch_bytes;
+} XmhMixJob;
+
+/* ---------- effects job ---------------------------------------------------- */
+typedef struct XmhFxJob {
+    int32_t channels;
+    int32_t n_clips;
+    int64_t frames;
+    const float *const *in_ptrs;   /* device array of n_clips device pointers */
+    float *const *out_ptrs;
+    const float *sos;              /* device n_sos x 6 */
+    int32_t n_sos;
+    int32_t fir_len;
+    const float *fir;              /* device fir_len taps */
+} XmhFxJob;
+
+/* ---------- runtime --------------------------------------------------------- */
+int  xmh_device_count(void);
+int  xmh_set_device(int dev);
+int  xmh_malloc(void **p, size_t bytes);
+void xmh_free(void *p);
+int  xmh_host_alloc(void **p, size_t bytes);   /* pinned */
+void xmh_host_free(void *p);
+int  xmh_stream_create(void **s);
+void xmh_stream_destroy(void *s);
+int  xmh_stream_sync(void *s);
+int  xmh_memcpy_h2d(void *dst, const void *src, size_t bytes, void *s);
+int  xmh_memcpy_d2h(void *dst, const void *src, size_t bytes, void *s);
+int  xmh_memcpy_d2d(void *dst, const void *src, size_t bytes, void *s);
+int  xmh_memset(void *dst, int v, size_t bytes, void *s);
+int  xmh_event_create(void **e);
+void xmh_event_destroy(void *e);
+int  xmh_event_record(void *e, void *s);
+int  xmh_event_elapsed(float *ms, void *e0, void *e1);  /* syncs e1 */
+int  xmh_pointer_is_device(const void *p);     /* 1 device, 0 host, <0 error */
+const char *xmh_arch_name(void);
+
+/* ---------- kernels ----------------------------------------------------------- */
+/* resample (if rs.L != rs.M) + gain + ordered track sum; returns launches made */
+int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches);
+int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
+/* synthetic PCM into device memory:
+ * clip c of n_clips at out + c*frames*channels samples, id = clip0 + c. */
+int xmh_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,
+              int channels, int64_t frames, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XM_SHIM_H */

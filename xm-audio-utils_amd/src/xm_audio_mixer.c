@@ -1,0 +1,507 @@
+/*
+ * xm_audio_mixer.c — the xm_audio_mixer_* C API (SURVEY.md §1 layers L3/L2):
+ * validation, handle state, host<->device staging, batch strides, and the
+ * dispatch into the HIP shim (csrc/xm_shim.h).  No arithmetic on samples
+ * happens here: every sample is produced by a gfx950 kernel, and a handle
+ * cannot be created without a usable GPU (no CPU fallback).
+ *
+ * Build-owned API (reference has none: /root/reference/README.md:1);
+ * contract in include/xm_audio_mixer.h and include/xm_audio_common.h.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "xm_internal.h"
+
+struct XmAudioMixer {
+    XmMixerConfig cfg;
+    int n_tracks;
+    XmTrackDesc tracks[XM_MAX_TRACKS];
+    XmhGain gains[XM_MAX_TRACKS];
+    XmhGain *gains_dev;
+    int gains_dirty;
+    int unity;                     /* single track, constant gain 1.0 */
+    XmTable table;
+    void *own_stream, *stream;
+    int user_stream;
+    void *ev[6];
+    XmMixerTiming timing;
+    /* device scratch */
+    void *d_in, *d_out, *d_fx;
+    size_t d_in_cap, d_out_cap, d_fx_cap;
+    void **d_ptrs;                 /* device pointer table (in ptrs then out ptrs) */
+    size_t d_ptrs_cap;
+    void **h_ptrs;                 /* pinned staging for the pointer table */
+    const XmEffects *fx;
+};
+
+static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
+
+static int grow(void **p, size_t *cap, size_t need)
+{
+    if (*cap >= need) return XM_OK;
+    xmh_free(*p);
+    *p = NULL;
+    *cap = 0;
+    size_t n = need + need / 8 + 4096;
+    int rc = xmh_malloc(p, n);
+    if (rc) return rc;
+    *cap = n;
+    return XM_OK;
+}
+
+XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status)
+{
+    int rc = XM_OK;
+    XmAudioMixer *m = NULL;
+    if (!cfg || cfg->in_rate <= 0 || cfg->out_rate <= 0 || (cfg->channels != 1 && cfg->channels != 2) ||
+        (cfg->sample_fmt != XM_FMT_S16 && cfg->sample_fmt != XM_FMT_F32) ||
+        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) || cfg->device < 0) {
+        rc = XM_EINVAL;
+        goto out;
+    }
+    if (cfg->device >= xmh_device_count()) {
+        rc = XM_EDEVICE;
+        goto out;
+    }
+    m = calloc(1, sizeof *m);
+    if (!m) {
+        rc = XM_ENOMEM;
+        goto out;
+    }
+    m->cfg = *cfg;
+    if ((rc = xmh_set_device(cfg->device))) goto out;
+    if ((rc = xm_table_build(&m->table, cfg->in_rate, cfg->out_rate))) goto out;
+    if ((rc = xmh_stream_create(&m->own_stream))) goto out;
+    m->stream = m->own_stream;
+    for (int i = 0; i < 6; ++i)
+        if ((rc = xmh_event_create(&m->ev[i]))) goto out;
+    if ((rc = xmh_malloc((void **)&m->gains_dev, sizeof(XmhGain) * XM_MAX_TRACKS))) goto out;
+    /* default: one track at unity gain */
+    XmTrackDesc t;
+    memset(&t, 0, sizeof t);
+    t.gain.gain0 = t.gain.gain1 = 1.0f;
+    t.gain.gain0_q15 = t.gain.gain1_q15 = 32768;
+    rc = xm_audio_mixer_set_tracks(m, &t, 1);
+out:
+    if (rc) xm_audio_mixer_freep(&m);
+    if (status) *status = rc;
+    return m;
+}
+
+XmAudioMixer *xm_audio_mixer_create(const XmMixerConfig *cfg) { return xm_audio_mixer_create_ex(cfg, NULL); }
+
+void xm_audio_mixer_freep(XmAudioMixer **pm)
+{
+    if (!pm || !*pm) return;
+    XmAudioMixer *m = *pm;
+    xmh_set_device(m->cfg.device);
+    if (m->own_stream) xmh_stream_sync(m->own_stream);
+    xm_table_free(&m->table);
+    xmh_free(m->gains_dev);
+    xmh_free(m->d_in);
+    xmh_free(m->d_out);
+    xmh_free(m->d_fx);
+    xmh_free(m->d_ptrs);
+    xmh_host_free(m->h_ptrs);
+    for (int i = 0; i < 6; ++i) xmh_event_destroy(m->ev[i]);
+    xmh_stream_destroy(m->own_stream);
+    free(m);
+    *pm = NULL;
+}
+
+int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_tracks)
+{
+    if (!m || !tracks || n_tracks < 1 || n_tracks > XM_MAX_TRACKS) return XM_EINVAL;
+    XmhGain g[XM_MAX_TRACKS];
+    for (int i = 0; i < n_tracks; ++i) {
+        if (tracks[i].in_rate != 0 && tracks[i].in_rate != m->cfg.in_rate) return XM_ENOSYS;
+        int rc = xm_gain_to_dev(&tracks[i].gain, &g[i]);
+        if (rc) return rc;
+    }
+    memcpy(m->tracks, tracks, sizeof(XmTrackDesc) * (size_t)n_tracks);
+    memcpy(m->gains, g, sizeof(XmhGain) * (size_t)n_tracks);
+    m->n_tracks = n_tracks;
+    m->gains_dirty = 1;
+    const XmhGain *g0 = &g[0];
+    int const_one = (g0->flags == 0) &&
+                    (m->cfg.sample_fmt == XM_FMT_F32 ? (g0->g0 == 1.0f && (g0->len == 0 ? g0->g1 == 1.0f
+                                                                                         : g0->g1 == 1.0f))
+                                                     : (g0->q0 == 32768 && g0->q1 == 32768));
+    m->unity = n_tracks == 1 && const_one;
+    return XM_OK;
+}
+
+int xm_audio_mixer_set_crossfade(XmAudioMixer *m, int from, int to, int64_t start, int64_t len)
+{
+    if (!m || from < 0 || to < 0 || from >= m->n_tracks || to >= m->n_tracks || from == to || len < 0)
+        return XM_EINVAL;
+    XmTrackDesc t[XM_MAX_TRACKS];
+    memcpy(t, m->tracks, sizeof(XmTrackDesc) * (size_t)m->n_tracks);
+    t[from].gain.mode = XM_GAIN_XFADE_OUT;
+    t[from].gain.ramp_start = start;
+    t[from].gain.ramp_len = len;
+    t[to].gain.mode = XM_GAIN_RAMP;
+    t[to].gain.gain0 = 0.0f;
+    t[to].gain.gain1 = 1.0f;
+    t[to].gain.gain0_q15 = 0;
+    t[to].gain.gain1_q15 = 32768;
+    t[to].gain.ramp_start = start;
+    t[to].gain.ramp_len = len;
+    return xm_audio_mixer_set_tracks(m, t, m->n_tracks);
+}
+
+int xm_audio_mixer_set_track_effects(XmAudioMixer *m, const XmEffects *fx)
+{
+    if (!m) return XM_EINVAL;
+    if (fx) {
+        if (m->cfg.sample_fmt != XM_FMT_F32) return XM_ENOSYS;
+        if (xm_effects_device(fx) != m->cfg.device) return XM_EINVAL;
+    }
+    m->fx = fx;
+    return XM_OK;
+}
+
+size_t xm_audio_mixer_out_frames(const XmAudioMixer *m, size_t frames_in)
+{
+    if (!m) return 0;
+    return xm_resample_out_frames(m->cfg.in_rate, m->cfg.out_rate, frames_in);
+}
+
+int xm_audio_mixer_set_stream(XmAudioMixer *m, void *s)
+{
+    if (!m) return XM_EINVAL;
+    m->stream = s ? s : m->own_stream;
+    m->user_stream = s != NULL;
+    return XM_OK;
+}
+
+int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t)
+{
+    if (!m || !t) return XM_EINVAL;
+    *t = m->timing;
+    return XM_OK;
+}
+
+/* ---- core: run one device-resident job ----------------------------------- */
+static void job_init(XmAudioMixer *m, XmhMixJob *j, size_t batch, size_t frames_in)
+{
+    memset(j, 0, sizeof *j);
+    j->fmt = m->cfg.sample_fmt;
+    j->channels = m->cfg.channels;
+    j->n_tracks = m->n_tracks;
+    j->n_mix = (int32_t)batch;
+    j->frames_in = (int64_t)frames_in;
+    j->frames_out = (int64_t)xm_audio_mixer_out_frames(m, frames_in);
+    j->gains = m->gains_dev;
+    j->unity = m->unity;
+    j->rs.L = m->table.d.L;
+    j->rs.M = m->table.d.M;
+    j->rs.T = m->table.d.T;
+    j->rs.rm = m->table.d.rm;
+    j->rs.H = m->table.H_dev;
+}
+
+static int upload_gains(XmAudioMixer *m)
+{
+    if (!m->gains_dirty) return XM_OK;
+    int rc = xmh_memcpy_h2d(m->gains_dev, m->gains, sizeof(XmhGain) * (size_t)m->n_tracks, m->stream);
+    if (!rc) rc = xmh_stream_sync(m->stream);   /* m->gains is host pageable memory */
+    if (!rc) m->gains_dirty = 0;
+    return rc;
+}
+
+/* Effects path (config 4): resample every track into scratch at unity gain,
+ * run the chain on each track in place, then the no-resample mix with the
+ * track gains.  Order per track: resample -> effects -> gain -> ordered sum. */
+static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
+{
+    const int C = j0->channels, ntr = j0->n_tracks;
+    const size_t per_track = (size_t)j0->frames_out * (size_t)C;
+    const size_t ntot = (size_t)j0->n_mix * (size_t)ntr;
+    int rc = grow(&m->d_fx, &m->d_fx_cap, ntot * per_track * sizeof(float) + 256);
+    if (rc) return rc;
+    float *scratch = (float *)m->d_fx;
+    /* 1) resample: treat every track as its own 1-track mix (unity gain) */
+    static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
+    XmhGain *ug = NULL;
+    rc = xmh_malloc((void **)&ug, sizeof unity_gain);
+    if (rc) return rc;
+    rc = xmh_memcpy_h2d(ug, &unity_gain, sizeof unity_gain, m->stream);
+    XmhMixJob r = *j0;
+    r.n_tracks = 1;
+    r.n_mix = (int32_t)ntot;
+    r.gains = ug;
+    r.unity = 1;
+    r.out = scratch;
+    r.out_ptrs = NULL;
+    r.out_mix_stride = (int64_t)per_track;
+    if (j0->in_ptrs) {
+        r.in_ptrs = j0->in_ptrs;   /* same mix-major order */
+    } else if (j0->in_mix_stride == (int64_t)ntr * j0->in_track_stride) {
+        r.in_mix_stride = j0->in_track_stride;
+        r.in_track_stride = 0;
+    } else {
+        rc = XM_ENOSYS;   /* irregular strides with effects: use process_batch */
+    }
+    if (!rc) rc = xmh_launch_mix(&r, m->stream, launches);
+    /* 2) effects chain on every track, in insertion order, in place */
+    const XmFxStage *st = NULL;
+    int ns = 0;
+    if (!rc) rc = xm_effects_stages(m->fx, &st, &ns);
+    void **tmp_ptrs = NULL;
+    if (!rc && ns > 0) {
+        rc = xmh_malloc((void **)&tmp_ptrs, sizeof(void *) * ntot * 2);
+        void **hp = malloc(sizeof(void *) * ntot * 2);
+        if (!hp) rc = XM_ENOMEM;
+        if (!rc) {
+            for (size_t i = 0; i < ntot; ++i) hp[i] = scratch + i * per_track;
+            rc = xmh_memcpy_h2d(tmp_ptrs, hp, sizeof(void *) * ntot, m->stream);
+            if (!rc) rc = xmh_stream_sync(m->stream);
+        }
+        free(hp);
+        for (int s = 0; !rc && s < ns; ++s) {
+            XmhFxJob fj;
+            memset(&fj, 0, sizeof fj);
+            fj.channels = C;
+            fj.n_clips = (int32_t)ntot;
+            fj.frames = j0->frames_out;
+            fj.in_ptrs = (const float *const *)tmp_ptrs;
+            fj.out_ptrs = (float *const *)tmp_ptrs;
+            if (st[s].kind == 1) {
+                fj.sos = st[s].coef_dev;
+                fj.n_sos = st[s].n;
+            } else {
+                rc = XM_ENOSYS;   /* FIR in-place needs a second buffer; biquad chains only */
+                break;
+            }
+            rc = xmh_launch_fx(&fj, m->stream, launches);
+        }
+    }
+    /* 3) mix, no resampling */
+    if (!rc) {
+        XmhMixJob x = *j0;
+        x.in = scratch;
+        x.in_ptrs = NULL;
+        x.in_track_stride = (int64_t)per_track;
+        x.in_mix_stride = (int64_t)(per_track * (size_t)ntr);
+        x.frames_in = j0->frames_out;
+        x.rs.L = x.rs.M = 1;
+        x.rs.T = 1;
+        x.rs.rm = 0;
+        x.unity = 0;
+        rc = xmh_launch_mix(&x, m->stream, launches);
+    }
+    xmh_stream_sync(m->stream);
+    xmh_free(tmp_ptrs);
+    xmh_free(ug);
+    return rc;
+}
+
+static int run_job(XmAudioMixer *m, XmhMixJob *j)
+{
+    int launches = 0;
+    int rc = xmh_event_record(m->ev[2], m->stream);
+    if (rc) return rc;
+    if (m->fx) rc = run_with_effects(m, j, &launches);
+    else rc = xmh_launch_mix(j, m->stream, &launches);
+    int rc2 = xmh_event_record(m->ev[3], m->stream);
+    m->timing.n_launches += launches;
+    return rc ? rc : rc2;
+}
+
+/* Detects in[b*ntr + tr] == base + (b*ms + tr*ts)*elem.  Returns 1 if strided. */
+static int as_strided(const void *const *p, size_t batch, int ntr, int elem, int64_t *ts, int64_t *ms)
+{
+    const char *base = (const char *)p[0];
+    int64_t t = 0, mm = 0;
+    if (ntr > 1) {
+        int64_t d = (const char *)p[1] - base;
+        if (d % elem) return 0;
+        t = d / elem;
+    }
+    if (batch > 1) {
+        int64_t d = (const char *)p[ntr] - base;
+        if (d % elem) return 0;
+        mm = d / elem;
+    }
+    for (size_t b = 0; b < batch; ++b)
+        for (int tr = 0; tr < ntr; ++tr)
+            if ((const char *)p[b * ntr + tr] != base + ((int64_t)b * mm + (int64_t)tr * t) * elem) return 0;
+    *ts = t;
+    *ms = mm;
+    return 1;
+}
+
+static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *const *out, size_t n_out,
+                     const void *const **din, void *const **dout)
+{
+    size_t n = n_in + n_out;
+    int rc;
+    if (m->d_ptrs_cap < n) {
+        xmh_free(m->d_ptrs);
+        xmh_host_free(m->h_ptrs);
+        m->d_ptrs = NULL;
+        m->h_ptrs = NULL;
+        m->d_ptrs_cap = 0;
+        if ((rc = xmh_malloc((void **)&m->d_ptrs, n * sizeof(void *)))) return rc;
+        if ((rc = xmh_host_alloc((void **)&m->h_ptrs, n * sizeof(void *)))) return rc;
+        m->d_ptrs_cap = n;
+    }
+    /* the previous call may still read the table on a user stream */
+    if ((rc = xmh_stream_sync(m->stream))) return rc;
+    if (in) memcpy(m->h_ptrs, in, n_in * sizeof(void *));
+    if (out) memcpy(m->h_ptrs + n_in, out, n_out * sizeof(void *));
+    if ((rc = xmh_memcpy_h2d(m->d_ptrs, m->h_ptrs, n * sizeof(void *), m->stream))) return rc;
+    *din = in ? (const void *const *)m->d_ptrs : NULL;
+    *dout = out ? (void *const *)(m->d_ptrs + n_in) : NULL;
+    return XM_OK;
+}
+
+static int finish(XmAudioMixer *m, int rc)
+{
+    if (!rc && !m->user_stream) rc = xmh_stream_sync(m->stream);
+    if (!rc && !m->user_stream) {
+        float ms = 0.0f;
+        if (!xmh_event_elapsed(&ms, m->ev[2], m->ev[3])) m->timing.kernel_ms = ms;
+    }
+    return rc;
+}
+
+static int process_device(XmAudioMixer *m, const void *const *in, void *const *out, size_t batch,
+                          size_t frames_in)
+{
+    XmhMixJob j;
+    job_init(m, &j, batch, frames_in);
+    const int elem = fmt_bytes(m->cfg.sample_fmt);
+    int64_t ts = 0, ms = 0, os = 0, dummy = 0;
+    const void *const *din = NULL;
+    void *const *dout = NULL;
+    int in_strided = as_strided(in, batch, m->n_tracks, elem, &ts, &ms);
+    int out_strided = as_strided((const void *const *)out, batch, 1, elem, &dummy, &os);
+    int rc = XM_OK;
+    if (!in_strided || !out_strided)
+        rc = ptr_table(m, in_strided ? NULL : in, in_strided ? 0 : batch * (size_t)m->n_tracks,
+                       out_strided ? NULL : out, out_strided ? 0 : batch, &din, &dout);
+    if (rc) return rc;
+    if (in_strided) {
+        j.in = in[0];
+        j.in_track_stride = ts;
+        j.in_mix_stride = ms;
+    } else {
+        j.in_ptrs = din;
+    }
+    if (out_strided) {
+        j.out = out[0];
+        j.out_mix_stride = os;
+    } else {
+        j.out_ptrs = dout;
+    }
+    return run_job(m, &j);
+}
+
+/* Host memory: stage mixes in chunks through device scratch, contiguous. */
+static int process_host(XmAudioMixer *m, const void *const *in, void *const *out, size_t batch,
+                        size_t frames_in)
+{
+    const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->n_tracks;
+    const size_t fout = xm_audio_mixer_out_frames(m, frames_in);
+    const size_t in_track = frames_in * (size_t)C * (size_t)elem;
+    const size_t out_mix = fout * (size_t)C * (size_t)elem;
+    const size_t per_mix = in_track * (size_t)ntr + out_mix;
+    size_t chunk = per_mix ? ((size_t)2 << 30) / per_mix : batch;   /* <= 2 GiB per chunk */
+    if (chunk < 1) chunk = 1;
+    if (chunk > batch) chunk = batch;
+    int rc = grow(&m->d_in, &m->d_in_cap, chunk * in_track * (size_t)ntr + 16);
+    if (!rc) rc = grow(&m->d_out, &m->d_out_cap, chunk * out_mix + 16);
+    float h2d = 0.0f, ker = 0.0f, d2h = 0.0f;
+    for (size_t b0 = 0; !rc && b0 < batch; b0 += chunk) {
+        size_t nb = batch - b0 < chunk ? batch - b0 : chunk;
+        rc = xmh_event_record(m->ev[0], m->stream);
+        for (size_t b = 0; !rc && b < nb; ++b)
+            for (int tr = 0; !rc && tr < ntr; ++tr)
+                rc = xmh_memcpy_h2d((char *)m->d_in + (b * (size_t)ntr + (size_t)tr) * in_track,
+                                    in[(b0 + b) * (size_t)ntr + (size_t)tr], in_track, m->stream);
+        if (rc) break;
+        XmhMixJob j;
+        job_init(m, &j, nb, frames_in);
+        j.in = m->d_in;
+        j.in_track_stride = (int64_t)(frames_in * (size_t)C);
+        j.in_mix_stride = j.in_track_stride * ntr;
+        j.out = m->d_out;
+        j.out_mix_stride = (int64_t)(fout * (size_t)C);
+        if ((rc = run_job(m, &j))) break;
+        for (size_t b = 0; !rc && b < nb; ++b)
+            rc = xmh_memcpy_d2h(out[b0 + b], (char *)m->d_out + b * out_mix, out_mix, m->stream);
+        if (!rc) rc = xmh_event_record(m->ev[4], m->stream);
+        if (!rc) rc = xmh_stream_sync(m->stream);
+        float a = 0, k = 0, c = 0;
+        if (!rc && !xmh_event_elapsed(&a, m->ev[0], m->ev[2])) h2d += a;
+        if (!rc && !xmh_event_elapsed(&k, m->ev[2], m->ev[3])) ker += k;
+        if (!rc && !xmh_event_elapsed(&c, m->ev[3], m->ev[4])) d2h += c;
+    }
+    m->timing.h2d_ms = h2d;
+    m->timing.kernel_ms = ker;
+    m->timing.d2h_ms = d2h;
+    return rc;
+}
+
+int xm_audio_mixer_process_batch(XmAudioMixer *m, const void *const *in, void *const *out, size_t batch,
+                                 size_t frames_in)
+{
+    if (!m || (batch && (!in || !out))) return XM_EINVAL;
+    if (batch == 0) return XM_OK;
+    if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    for (size_t i = 0; i < batch * (size_t)m->n_tracks; ++i)
+        if (!in[i]) return XM_EINVAL;
+    for (size_t i = 0; i < batch; ++i)
+        if (!out[i]) return XM_EINVAL;
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    memset(&m->timing, 0, sizeof m->timing);
+    if ((rc = upload_gains(m))) return rc;
+    if (xm_audio_mixer_out_frames(m, frames_in) == 0) return XM_OK;
+    if (m->cfg.mem_kind == XM_MEM_DEVICE) rc = process_device(m, in, out, batch, frames_in);
+    else rc = process_host(m, in, out, batch, frames_in);
+    return finish(m, rc);
+}
+
+int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in_track_stride,
+                                   ptrdiff_t in_mix_stride, void *out, ptrdiff_t out_mix_stride, size_t batch,
+                                   size_t frames_in)
+{
+    if (!m || (batch && (!in || !out))) return XM_EINVAL;
+    if (batch == 0) return XM_OK;
+    if (m->cfg.mem_kind != XM_MEM_DEVICE) {
+        /* host memory: expand to pointer arrays */
+        const int elem = fmt_bytes(m->cfg.sample_fmt);
+        size_t ntr = (size_t)m->n_tracks;
+        const void **ip = malloc(sizeof(void *) * batch * ntr);
+        void **op = malloc(sizeof(void *) * batch);
+        int rc = (!ip || !op) ? XM_ENOMEM : XM_OK;
+        for (size_t b = 0; !rc && b < batch; ++b) {
+            for (size_t tr = 0; tr < ntr; ++tr)
+                ip[b * ntr + tr] = (const char *)in + ((ptrdiff_t)b * in_mix_stride + (ptrdiff_t)tr * in_track_stride) * elem;
+            op[b] = (char *)out + (ptrdiff_t)b * out_mix_stride * elem;
+        }
+        if (!rc) rc = xm_audio_mixer_process_batch(m, (const void *const *)ip, (void *const *)op, batch, frames_in);
+        free(ip);
+        free(op);
+        return rc;
+    }
+    if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    memset(&m->timing, 0, sizeof m->timing);
+    if ((rc = upload_gains(m))) return rc;
+    if (xm_audio_mixer_out_frames(m, frames_in) == 0) return XM_OK;
+    XmhMixJob j;
+    job_init(m, &j, batch, frames_in);
+    j.in = in;
+    j.in_track_stride = in_track_stride;
+    j.in_mix_stride = in_mix_stride;
+    j.out = out;
+    j.out_mix_stride = out_mix_stride;
+    rc = run_job(m, &j);
+    return finish(m, rc);
+}

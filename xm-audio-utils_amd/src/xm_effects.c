@@ -1,0 +1,372 @@
+/*
+ * xm_effects.c — the xm_effects_* C API: chain construction (biquad sections,
+ * RBJ EQ bands designed in fp64, FIR taps), staging and dispatch of the
+ * gfx950 effects kernels (csrc/xm_fx.hip).  Build-owned API (reference has
+ * none: /root/reference/README.md:1); contract in include/xm_effects.h.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "xm_internal.h"
+
+struct XmEffects {
+    XmEffectsConfig cfg;
+    int n_effects;
+    struct {
+        int kind;          /* 1 biquad section, 2 FIR */
+        int n;             /* taps for FIR */
+        float sos[6];
+        float *fir;        /* host copy */
+    } fx[XM_MAX_EFFECTS];
+    XmFxStage stages[XM_MAX_EFFECTS];
+    int n_stages;
+    int dirty;
+    void *own_stream, *stream;
+    int user_stream;
+    void *d_buf[2];
+    size_t d_cap[2];
+    void **d_ptrs;
+    void **h_ptrs;
+    size_t ptr_cap;
+};
+
+XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status)
+{
+    int rc = XM_OK;
+    XmEffects *e = NULL;
+    if (!cfg || cfg->rate <= 0 || (cfg->channels != 1 && cfg->channels != 2) ||
+        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) || cfg->device < 0) {
+        rc = XM_EINVAL;
+        goto out;
+    }
+    if (cfg->device >= xmh_device_count()) {
+        rc = XM_EDEVICE;
+        goto out;
+    }
+    e = calloc(1, sizeof *e);
+    if (!e) {
+        rc = XM_ENOMEM;
+        goto out;
+    }
+    e->cfg = *cfg;
+    if ((rc = xmh_set_device(cfg->device))) goto out;
+    if ((rc = xmh_stream_create(&e->own_stream))) goto out;
+    e->stream = e->own_stream;
+out:
+    if (rc) xm_effects_freep(&e);
+    if (status) *status = rc;
+    return e;
+}
+
+XmEffects *xm_effects_create(int rate, int channels, int n_devices)
+{
+    if (n_devices != 1) return NULL;
+    XmEffectsConfig c = {rate, channels, XM_MEM_HOST, 0};
+    return xm_effects_create_ex(&c, NULL);
+}
+
+static void free_stages(XmEffects *e)
+{
+    for (int i = 0; i < e->n_stages; ++i) xmh_free(e->stages[i].coef_dev);
+    e->n_stages = 0;
+}
+
+void xm_effects_freep(XmEffects **pe)
+{
+    if (!pe || !*pe) return;
+    XmEffects *e = *pe;
+    xmh_set_device(e->cfg.device);
+    if (e->own_stream) xmh_stream_sync(e->own_stream);
+    free_stages(e);
+    for (int i = 0; i < e->n_effects; ++i) free(e->fx[i].fir);
+    xmh_free(e->d_buf[0]);
+    xmh_free(e->d_buf[1]);
+    xmh_free(e->d_ptrs);
+    xmh_host_free(e->h_ptrs);
+    xmh_stream_destroy(e->own_stream);
+    free(e);
+    *pe = NULL;
+}
+
+int xm_effects_add_biquad(XmEffects *e, const float sos[6])
+{
+    if (!e || !sos) return XM_EINVAL;
+    if (sos[3] != 1.0f) return XM_EINVAL;   /* scipy sosfilt requires a0 == 1 */
+    for (int i = 0; i < 6; ++i)
+        if (!isfinite(sos[i])) return XM_EINVAL;
+    if (e->n_effects >= XM_MAX_EFFECTS) return XM_ENOMEM;
+    /* a cascade longer than XM_MAX_SOS sections is split by the stager */
+    e->fx[e->n_effects].kind = 1;
+    memcpy(e->fx[e->n_effects].sos, sos, sizeof(float) * 6);
+    e->n_effects++;
+    e->dirty = 1;
+    return XM_OK;
+}
+
+/* RBJ audio-EQ-cookbook (R. Bristow-Johnson), fp64, normalised by a0, cast to
+ * fp32.  Mirrored by oracle/np_oracle.py:rbj_section for the parity tests. */
+int xm_effects_add_eq_band(XmEffects *e, int band, double f0, double gain_db, double q)
+{
+    if (!e || f0 <= 0.0 || f0 >= 0.5 * e->cfg.rate || q <= 0.0 || !isfinite(gain_db)) return XM_EINVAL;
+    const double A = pow(10.0, gain_db / 40.0);
+    const double w0 = 2.0 * 3.141592653589793 * f0 / (double)e->cfg.rate;
+    const double cw = cos(w0), sw = sin(w0);
+    double alpha, b[3], a[3];
+    if (band == XM_EQ_LOWSHELF || band == XM_EQ_HIGHSHELF)
+        alpha = sw / 2.0 * sqrt((A + 1.0 / A) * (1.0 / q - 1.0) + 2.0);
+    else
+        alpha = sw / (2.0 * q);
+    switch (band) {
+    case XM_EQ_PEAKING:
+        b[0] = 1 + alpha * A; b[1] = -2 * cw; b[2] = 1 - alpha * A;
+        a[0] = 1 + alpha / A; a[1] = -2 * cw; a[2] = 1 - alpha / A;
+        break;
+    case XM_EQ_LOWSHELF: {
+        const double sa = 2 * sqrt(A) * alpha;
+        b[0] = A * ((A + 1) - (A - 1) * cw + sa); b[1] = 2 * A * ((A - 1) - (A + 1) * cw);
+        b[2] = A * ((A + 1) - (A - 1) * cw - sa);
+        a[0] = (A + 1) + (A - 1) * cw + sa; a[1] = -2 * ((A - 1) + (A + 1) * cw);
+        a[2] = (A + 1) + (A - 1) * cw - sa;
+        break;
+    }
+    case XM_EQ_HIGHSHELF: {
+        const double sa = 2 * sqrt(A) * alpha;
+        b[0] = A * ((A + 1) + (A - 1) * cw + sa); b[1] = -2 * A * ((A - 1) + (A + 1) * cw);
+        b[2] = A * ((A + 1) + (A - 1) * cw - sa);
+        a[0] = (A + 1) - (A - 1) * cw + sa; a[1] = 2 * ((A - 1) - (A + 1) * cw);
+        a[2] = (A + 1) - (A - 1) * cw - sa;
+        break;
+    }
+    case XM_EQ_LOWPASS:
+        b[0] = (1 - cw) / 2; b[1] = 1 - cw; b[2] = (1 - cw) / 2;
+        a[0] = 1 + alpha; a[1] = -2 * cw; a[2] = 1 - alpha;
+        break;
+    case XM_EQ_HIGHPASS:
+        b[0] = (1 + cw) / 2; b[1] = -(1 + cw); b[2] = (1 + cw) / 2;
+        a[0] = 1 + alpha; a[1] = -2 * cw; a[2] = 1 - alpha;
+        break;
+    default:
+        return XM_EINVAL;
+    }
+    const float sos[6] = {(float)(b[0] / a[0]), (float)(b[1] / a[0]), (float)(b[2] / a[0]), 1.0f,
+                          (float)(a[1] / a[0]), (float)(a[2] / a[0])};
+    return xm_effects_add_biquad(e, sos);
+}
+
+int xm_effects_add_fir(XmEffects *e, const float *h, int K)
+{
+    if (!e || !h || K < 1 || K > XM_MAX_FIR) return XM_EINVAL;
+    if (e->n_effects >= XM_MAX_EFFECTS) return XM_ENOMEM;
+    float *c = malloc(sizeof(float) * (size_t)K);
+    if (!c) return XM_ENOMEM;
+    memcpy(c, h, sizeof(float) * (size_t)K);
+    e->fx[e->n_effects].kind = 2;
+    e->fx[e->n_effects].n = K;
+    e->fx[e->n_effects].fir = c;
+    e->n_effects++;
+    e->dirty = 1;
+    return XM_OK;
+}
+
+int xm_effects_count(const XmEffects *e) { return e ? e->n_effects : XM_EINVAL; }
+
+int xm_effects_get_biquad(const XmEffects *e, int i, float sos[6])
+{
+    if (!e || !sos || i < 0 || i >= e->n_effects || e->fx[i].kind != 1) return XM_EINVAL;
+    memcpy(sos, e->fx[i].sos, sizeof(float) * 6);
+    return XM_OK;
+}
+
+int xm_effects_set_stream(XmEffects *e, void *s)
+{
+    if (!e) return XM_EINVAL;
+    e->stream = s ? s : e->own_stream;
+    e->user_stream = s != NULL;
+    return XM_OK;
+}
+
+int xm_effects_device(const XmEffects *e) { return e ? e->cfg.device : -1; }
+
+/* Group consecutive biquads into cascades (<= XM_MAX_SOS sections each) and
+ * upload coefficients. */
+static int build_stages(XmEffects *e)
+{
+    if (!e->dirty) return XM_OK;
+    xmh_set_device(e->cfg.device);
+    free_stages(e);
+    int rc = XM_OK;
+    for (int i = 0; !rc && i < e->n_effects;) {
+        XmFxStage *s = &e->stages[e->n_stages];
+        if (e->fx[i].kind == 1) {
+            float buf[6 * XM_MAX_SOS];
+            int n = 0;
+            while (i < e->n_effects && e->fx[i].kind == 1 && n < XM_MAX_SOS) {
+                memcpy(buf + 6 * n, e->fx[i].sos, sizeof(float) * 6);
+                ++n;
+                ++i;
+            }
+            s->kind = 1;
+            s->n = n;
+            rc = xmh_malloc((void **)&s->coef_dev, sizeof(float) * 6 * (size_t)n);
+            if (!rc) rc = xmh_memcpy_h2d(s->coef_dev, buf, sizeof(float) * 6 * (size_t)n, e->stream);
+        } else {
+            s->kind = 2;
+            s->n = e->fx[i].n;
+            rc = xmh_malloc((void **)&s->coef_dev, sizeof(float) * (size_t)s->n);
+            if (!rc) rc = xmh_memcpy_h2d(s->coef_dev, e->fx[i].fir, sizeof(float) * (size_t)s->n, e->stream);
+            ++i;
+        }
+        if (!rc) e->n_stages++;
+    }
+    if (!rc) rc = xmh_stream_sync(e->stream);
+    if (!rc) e->dirty = 0;
+    return rc;
+}
+
+int xm_effects_stages(const XmEffects *ce, const XmFxStage **stages, int *n)
+{
+    XmEffects *e = (XmEffects *)ce;   /* lazily built cache */
+    int rc = build_stages(e);
+    if (rc) return rc;
+    *stages = e->stages;
+    *n = e->n_stages;
+    return XM_OK;
+}
+
+static int grow(void **p, size_t *cap, size_t need)
+{
+    if (*cap >= need) return XM_OK;
+    xmh_free(*p);
+    *p = NULL;
+    *cap = 0;
+    int rc = xmh_malloc(p, need);
+    if (!rc) *cap = need;
+    return rc;
+}
+
+static int ensure_ptrs(XmEffects *e, size_t n)
+{
+    if (e->ptr_cap >= n) return XM_OK;
+    xmh_free(e->d_ptrs);
+    xmh_host_free(e->h_ptrs);
+    e->d_ptrs = NULL;
+    e->h_ptrs = NULL;
+    e->ptr_cap = 0;
+    int rc = xmh_malloc((void **)&e->d_ptrs, n * sizeof(void *));
+    if (!rc) rc = xmh_host_alloc((void **)&e->h_ptrs, n * sizeof(void *));
+    if (!rc) e->ptr_cap = n;
+    return rc;
+}
+
+/* Runs every stage; ping-pong through two device buffers so FIR never reads
+ * what it writes.  src/dst: device pointer tables (n clips each). */
+static int run_chain(XmEffects *e, size_t batch, size_t frames, float **src, float **dst)
+{
+    const int C = e->cfg.channels;
+    const size_t per = frames * (size_t)C;
+    int rc = grow(&e->d_buf[0], &e->d_cap[0], batch * per * sizeof(float) + 16);
+    if (!rc) rc = grow(&e->d_buf[1], &e->d_cap[1], batch * per * sizeof(float) + 16);
+    if (!rc) rc = ensure_ptrs(e, batch * 6);
+    if (rc) return rc;
+    rc = xmh_stream_sync(e->stream);
+    if (rc) return rc;
+    /* table layout: [0,b) src  [b,2b) dst  [2b,3b) buf0  [3b,4b) buf1 */
+    for (size_t i = 0; i < batch; ++i) {
+        e->h_ptrs[i] = src[i];
+        e->h_ptrs[batch + i] = dst[i];
+        e->h_ptrs[2 * batch + i] = (float *)e->d_buf[0] + i * per;
+        e->h_ptrs[3 * batch + i] = (float *)e->d_buf[1] + i * per;
+    }
+    rc = xmh_memcpy_h2d(e->d_ptrs, e->h_ptrs, 4 * batch * sizeof(void *), e->stream);
+    if (rc) return rc;
+    void **T_src = e->d_ptrs, **T_dst = e->d_ptrs + batch;
+    void **T_b[2] = {e->d_ptrs + 2 * batch, e->d_ptrs + 3 * batch};
+    int launches = 0;
+    if (e->n_stages == 0) {
+        for (size_t i = 0; !rc && i < batch; ++i)
+            if (src[i] != dst[i]) rc = xmh_memcpy_d2d(dst[i], src[i], per * sizeof(float), e->stream);
+        return rc;
+    }
+    /* FIR reads neighbours of the samples it writes: never run it in place.
+     * If any clip is processed in place, first copy the inputs to buf0. */
+    int inplace = 0, off = 0;
+    for (size_t i = 0; i < batch; ++i) inplace |= src[i] == dst[i];
+    void **cur = T_src;
+    if (inplace) {
+        for (size_t i = 0; !rc && i < batch; ++i)
+            rc = xmh_memcpy_d2d((float *)e->d_buf[0] + i * per, src[i], per * sizeof(float), e->stream);
+        cur = T_b[0];
+        off = 1;
+    }
+    for (int s = 0; !rc && s < e->n_stages; ++s) {
+        const int last = s == e->n_stages - 1;
+        void **nxt = last ? T_dst : T_b[(s + off) & 1];
+        XmhFxJob j;
+        memset(&j, 0, sizeof j);
+        j.channels = C;
+        j.n_clips = (int32_t)batch;
+        j.frames = (int64_t)frames;
+        j.in_ptrs = (const float *const *)cur;
+        j.out_ptrs = (float *const *)nxt;
+        if (e->stages[s].kind == 1) {
+            j.sos = e->stages[s].coef_dev;
+            j.n_sos = e->stages[s].n;
+        } else {
+            j.fir = e->stages[s].coef_dev;
+            j.fir_len = e->stages[s].n;
+        }
+        rc = xmh_launch_fx(&j, e->stream, &launches);
+        cur = nxt;
+    }
+    return rc;
+}
+
+int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const *out, size_t batch, size_t frames)
+{
+    if (!e || (batch && (!in || !out))) return XM_EINVAL;
+    if (batch == 0 || frames == 0) return XM_OK;
+    if (batch > (size_t)INT32_MAX / 2) return XM_EINVAL;
+    int rc = xmh_set_device(e->cfg.device);
+    if (!rc) rc = build_stages(e);
+    if (rc) return rc;
+    const size_t bytes = frames * (size_t)e->cfg.channels * sizeof(float);
+    if (e->cfg.mem_kind == XM_MEM_DEVICE) {
+        /* FIR stages must not run in place: route through scratch when in == out */
+        float **src = malloc(sizeof(float *) * batch), **dst = malloc(sizeof(float *) * batch);
+        if (!src || !dst) rc = XM_ENOMEM;
+        for (size_t i = 0; !rc && i < batch; ++i) {
+            src[i] = (float *)in[i];
+            dst[i] = out[i];
+        }
+        if (!rc) rc = run_chain(e, batch, frames, src, dst);
+        free(src);
+        free(dst);
+    } else {
+        /* host: stage through a device buffer (chunks of <= 1 GiB) */
+        size_t chunk = bytes ? ((size_t)1 << 30) / bytes : batch;
+        if (chunk < 1) chunk = 1;
+        if (chunk > batch) chunk = batch;
+        void *d_io = NULL;
+        rc = xmh_malloc(&d_io, chunk * bytes * 2);
+        float **src = malloc(sizeof(float *) * chunk), **dst = malloc(sizeof(float *) * chunk);
+        if (!src || !dst) rc = XM_ENOMEM;
+        for (size_t b0 = 0; !rc && b0 < batch; b0 += chunk) {
+            size_t nb = batch - b0 < chunk ? batch - b0 : chunk;
+            for (size_t i = 0; !rc && i < nb; ++i) {
+                src[i] = (float *)d_io + i * (bytes / sizeof(float));
+                dst[i] = (float *)d_io + (chunk + i) * (bytes / sizeof(float));
+                rc = xmh_memcpy_h2d(src[i], in[b0 + i], bytes, e->stream);
+            }
+            if (!rc) rc = run_chain(e, nb, frames, src, dst);
+            for (size_t i = 0; !rc && i < nb; ++i) rc = xmh_memcpy_d2h(out[b0 + i], dst[i], bytes, e->stream);
+            if (!rc) rc = xmh_stream_sync(e->stream);
+        }
+        free(src);
+        free(dst);
+        xmh_stream_sync(e->stream);
+        xmh_free(d_io);
+    }
+    if (!rc && !e->user_stream) rc = xmh_stream_sync(e->stream);
+    return rc;
+}
