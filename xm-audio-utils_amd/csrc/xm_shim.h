@@ -55,6 +55,7 @@ typedef struct XmhMixJob {
     int64_t out_mix_stride;
     void *const *out_ptrs;
     const XmhGain *gains;     /* device, n_tracks entries */
+    const XmhGain *gains_host; /* host copy (kernel-argument path), n_tracks entries */
     int32_t unity;            /* 1: every gain is constant 1.0 (pure resample fast path) */
     int32_t reserved;
     XmhResample rs;
@@ -104,6 +105,9 @@ const char *xmh_arch_name(void);
 /* resample (if rs.L != rs.M) + gain + ordered track sum; returns launches made */
 int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches);
 int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
+/* k-ordered coefficient table for the 147/160 fast kernel; -1003 if H does
+ * not qualify (tap 22 of some phase non-zero) */
+int xmh_fast_table_147_160(const float *H, int T, float *Hk);
 /* synthetic PCM into device memory:
  * clip c of n_clips at out + c*frames*channels samples, id = clip0 + c. */
 int xmh_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,

@@ -194,12 +194,14 @@ static void job_init(XmAudioMixer *m, XmhMixJob *j, size_t batch, size_t frames_
     j->frames_in = (int64_t)frames_in;
     j->frames_out = (int64_t)xm_audio_mixer_out_frames(m, frames_in);
     j->gains = m->gains_dev;
+    j->gains_host = m->gains;
     j->unity = m->unity;
     j->rs.L = m->table.d.L;
     j->rs.M = m->table.d.M;
     j->rs.T = m->table.d.T;
     j->rs.rm = m->table.d.rm;
     j->rs.H = m->table.H_dev;
+    j->rs.Hrun = m->table.Hk_dev;
 }
 
 static int upload_gains(XmAudioMixer *m)
@@ -232,6 +234,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     r.n_tracks = 1;
     r.n_mix = (int32_t)ntot;
     r.gains = ug;
+    r.gains_host = &unity_gain;
     r.unity = 1;
     r.out = scratch;
     r.out_ptrs = NULL;
@@ -290,6 +293,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         x.rs.T = 1;
         x.rs.rm = 0;
         x.unity = 0;
+        x.rs.Hrun = NULL;
         rc = xmh_launch_mix(&x, m->stream, launches);
     }
     xmh_stream_sync(m->stream);

@@ -195,6 +195,17 @@ int xm_table_build(XmTable *t, int in_rate, int out_rate)
     rc = xm_resample_design(in_rate, out_rate, &t->d, H);
     if (!rc) rc = xmh_malloc((void **)&t->H_dev, n * sizeof(float));
     if (!rc) rc = xmh_memcpy_h2d(t->H_dev, H, n * sizeof(float), NULL);
+    if (!rc && t->d.L == 147 && t->d.M == 160) {
+        /* specialised 48k->44.1k kernel table (csrc/xm_resample_fast.hip) */
+        float *Hk = malloc(sizeof(float) * 147 * 24);
+        if (!Hk) rc = XM_ENOMEM;
+        if (!rc && xmh_fast_table_147_160(H, t->d.T, Hk) == 0) {
+            rc = xmh_malloc((void **)&t->Hk_dev, sizeof(float) * 147 * 24);
+            if (!rc) rc = xmh_memcpy_h2d(t->Hk_dev, Hk, sizeof(float) * 147 * 24, NULL);
+        }
+        if (!rc) rc = xmh_stream_sync(NULL);
+        free(Hk);
+    }
     if (!rc) rc = xmh_stream_sync(NULL);
     free(H);
     if (rc) xm_table_free(t);
@@ -204,7 +215,9 @@ int xm_table_build(XmTable *t, int in_rate, int out_rate)
 void xm_table_free(XmTable *t)
 {
     xmh_free(t->H_dev);
+    xmh_free(t->Hk_dev);
     t->H_dev = NULL;
+    t->Hk_dev = NULL;
 }
 
 int xm_gain_to_dev(const XmGainRamp *g, XmhGain *d)

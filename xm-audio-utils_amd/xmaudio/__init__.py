@@ -17,6 +17,17 @@ import os
 
 import numpy as np
 
+# PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as
+# /opt/rocm's).  The first one loaded in a process is the one every later
+# library binds to, and torch refuses to initialise on a runtime it did not
+# load itself ("No HIP GPUs are available").  So when torch is installed,
+# load it first: libxm_audio.so then binds to torch's runtime and both share
+# one HIP context (device memory, streams) in the same process.
+try:  # pragma: no cover - environment dependent
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libxm_audio.so")
 if not os.path.exists(LIB_PATH):
