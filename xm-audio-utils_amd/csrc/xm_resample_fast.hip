@@ -5,89 +5,97 @@
 // Arithmetic is scipy resample_poly's (include/xm_audio_common.h): per output
 // acc = sum_t x[j0+t]*H[ph][t] in ascending t, each mul and add rounded
 // separately (-ffp-contract=off), then mix = ((+0 + g0*r0) + g1*r1) + ...
-// Two exact shortcuts, both argued in DESIGN.md §"Exactness of the fast path":
+// Exact shortcuts (DESIGN.md §"Exactness of the fast path"):
 //  * tap 22 of every phase is an exact 0 for 147/160 (the 160-zero pre-pad),
 //    so each output uses taps 0..21 (finite inputs);
 //  * the +0 seeds of the dot product and of the mix are folded into one
-//    final "+ 0.0f", which maps -0 to +0 and leaves every other value alone.
+//    final "+ 0.0f", which maps -0 to +0 and leaves every other value alone;
+//  * inside a ramp g = gA + gS*(float)k with (gA, gS) = (g0, step) or, for a
+//    crossfade-out, (1, -step): 1 + (-step)*k == 1 - (0 + step*k) bit for bit.
 //
-// Work decomposition (MI355X-first):
-//  * super-period (SP) = 160 input frames -> 147 output frames; the filter
+// Work decomposition (MI355X-first; measurements in DESIGN.md §fast kernel):
+//  * super-period (SP) = 160 input frames -> 147 output frames.  The filter
 //    phase of output k of an SP does not depend on the SP, so a wave whose
-//    64 lanes hold 64 consecutive SPs of ONE track runs a wave-uniform phase
-//    sequence: the 22 coefficients of every output come from the scalar
-//    cache as SGPR operands of v_pk_mul_f32 (stereo L/R packed), never from
-//    VGPRs or LDS;
-//  * the SP's 147 outputs are fully unrolled, so the sliding window over the
-//    lane's 186 input frames is a static register window: every input frame
-//    is loaded once (16-B buffer loads, 4 back-to-back per 64-B sector) and
-//    used by up to 22 outputs from registers;
-//  * buffer-resource range checking zero-fills frames outside [0, N): no
-//    branches for clip edges (the lane holding SP 0 points its first 8
-//    loads out of range);
-//  * a workgroup = NT track waves x (8/NT) SP groups.  Each round of 8
-//    outputs the waves exchange gain*r through a 32 KiB LDS buffer (double
-//    buffered), one barrier, and every lane adds one output's NT tracks in
-//    track order — the mix never touches HBM as partial sums.
+//    64 lanes are 64 SP streams runs one wave-uniform phase sequence: the 22
+//    coefficients of each output are SGPR operands (scalar cache) of
+//    v_pk_mul_f32 on stereo L/R pairs.
+//  * lanes = NT tracks x S (=64/NT) stream slots of one mix.  Each lane walks
+//    R consecutive SPs of its track, so its input is one contiguous stream
+//    and the register window carries across SPs (43 frames moved per SP).
+//  * input arrives by LDS-DMA (buffer_load ... lds) in 256-B segments per
+//    stream: one DMA instruction = 4 streams x 256 B.  Measured on MI355X
+//    (tools/ubench/mem_pattern.hip): 16 lanes per 256-B segment streams at
+//    6.3 TB/s, whereas one 16-B stream per lane caps at 4.2 TB/s.  Chunks
+//    are rotated per stream so the LDS->VGPR copy (ds_read_b128) is
+//    bank-conflict free; buffer range checks plus explicit redirects
+//    zero-fill frames outside [0, N).
+//  * the ordered track sum is exchanged through 4 KiB of wave-private LDS
+//    (rows rotated instead of padded): no workgroup barriers at all.
+//  * LDS per wave = 16 KiB slot + 4 KiB exchange = 20 KiB -> 8 waves/CU,
+//    leaving a 256-VGPR budget for the window.
+#include <stdlib.h>
 #include <string.h>
 #include "xm_device.h"
 
 namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
-// Coefficients are read through the constant address space: wave-uniform
-// addresses there always lower to s_load (scalar cache -> SGPR operands).
-typedef const float __attribute__((address_space(4))) cfloat;
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef const float __attribute__((address_space(4))) cfloat;   // -> s_load
+typedef const f2 __attribute__((address_space(4))) cf2;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int L = 147, M = 160, RM = 11;   // reduced ratio, output offset rm
 constexpr int TE = 22;                     // taps used (tap 22 is an exact zero)
 constexpr int SPO = L;                     // outputs per super-period
 constexpr int SPI = M;                     // input frames per super-period
-constexpr int F0 = -16;                    // first loaded frame, relative to 160*sp
+constexpr int SEGF = 32;                   // frames per DMA segment (256 B)
 constexpr int G = 8;                       // outputs per exchange round
 constexpr int ROUNDS = (SPO + G - 1) / G;  // 19
-constexpr int WAVES = 8;                   // waves per workgroup
 constexpr int HK_STRIDE = 24;              // floats per output row of the k-ordered table
+constexpr int CARRY0 = 21;                 // first rel frame an SP needs
+constexpr int WIN = 7 * SEGF;              // 224 rel frames: SP s uses rel [21, 201]
+constexpr int SLOT_BYTES = 64 * 256;       // one segment for 64 streams
+constexpr int X_F2 = G * 64;               // exchange: 8 outputs x 64 lanes (f2)
+constexpr int LDS_PER_WAVE = SLOT_BYTES + X_F2 * 8;   // 20 KiB
+constexpr uint32_t OOB = 0x80000000u;      // voffset beyond every num_records
 
-// Input frame (relative to 160*sp + F0) of tap 0 for output k of an SP.
-// (scipy: j0 = floor((m+rm)*M/L) - T + 1 with T = 23; relative to 160*sp + F0)
-__host__ __device__ constexpr int rk(int k) { return ((k + RM) * M) / L - 22 - F0; }
-// last pair (16 B = 2 frames) needed by outputs [0, k]
-constexpr int last_pair(int k) { return (rk(k) + TE - 1) / 2; }
-constexpr int first_pair() { return rk(0) / 2; }
-constexpr int NPAIR = last_pair(SPO - 1) + 1;                   // 93 pairs = 186 frames
-static_assert(rk(0) == 5, "window origin");
-static_assert(NPAIR == 93, "pairs per SP");
+// rel frame (relative to 160*s - 32) of tap 0 of output k of SP s
+// (scipy: j0 = floor((m+rm)*M/L) - T + 1, T = 23)
+__host__ __device__ constexpr int rk(int k) { return ((k + RM) * M) / L - 22 + 32; }
+// segment (0..6 of the SP's 7) holding the last frame output k needs
+constexpr int last_seg(int k) { return (rk(k) + TE - 1) / SEGF; }
+// last segment needed by the pair starting at even k / before it
+constexpr int need_pair(int k) { return last_seg(k + 1 < SPO ? k + 1 : k); }
+constexpr int need_before(int k) { return k == 0 ? 1 : last_seg(k - 1); }
+static_assert(rk(0) == CARRY0, "window origin");
+static_assert(last_seg(SPO - 1) == 6, "an SP spans 7 segments");
+static_assert(last_seg(0) == 1, "first outputs need segments 0,1");
 
 struct FastArgs {
-    const float *in;
-    int64_t in_track_stride, in_mix_stride;     // floats
-    const void *const *in_ptrs;
+    const float *in;                 // mix 0, track 0
+    int64_t in_mix_stride;           // floats
+    int64_t track_bytes;             // bytes between tracks of a mix (>= 8*N)
     float *out;
-    int64_t out_mix_stride;                     // floats
-    void *const *out_ptrs;
-    const float *Hk;                            // [147][24] coefficients in output order
+    int64_t out_mix_stride;          // floats
+    const float *Hk;                 // [147][24] coefficients in output order
     int32_t n_mix, n_tracks;
     int32_t frames_in, frames_out;
-    int32_t n_sp, groups_per_mix;
+    int32_t n_sp;                    // SPs per clip = ceil(frames_out / 147)
+    int32_t R;                       // SPs per lane (consecutive)
+    int32_t tasks_per_mix;
     int32_t unity;
-    int32_t pad;
     XmhGain g[8];
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes)
 {
-    // stride 0, num_records = bytes, default dword format flags for gfx950 raw buffers
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-__device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm)
-{
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff + imm, 0, 0));
-}
-
-// exact per-output gain (xm_device.h::xm_gain_f32 with wave-uniform params)
-__device__ __forceinline__ float gain_at(const XmhGain &g, int n)
+// exact contract gain (xm_audio_common.h) at output frame n
+__device__ __forceinline__ float gain_exact(const XmhGain &g, int n)
 {
     float v;
     if (g.len == 0) {
@@ -100,182 +108,296 @@ __device__ __forceinline__ float gain_at(const XmhGain &g, int n)
     return (g.flags & XMH_GAIN_XFADE_OUT) ? 1.0f - v : v;
 }
 
-template <int NT, bool UNITY>
-__global__ __launch_bounds__(512) void k_rs147_mix(FastArgs a)
+template <int NT>
+__global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
 {
-    extern __shared__ __attribute__((aligned(16))) f2 xbuf[];   // [2][G][NT][SPWG]
-    constexpr int SPG = WAVES / NT;            // SP groups per workgroup
-    constexpr int SPWG = 64 * SPG;             // SPs per workgroup
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tr = w % NT;                     // this wave's track
-    const int grp = w / NT;                    // this wave's SP group within the WG
-    const int mix = blockIdx.x / a.groups_per_mix;
-    const int wg_sp0 = (blockIdx.x % a.groups_per_mix) * SPWG;
-    const int sp_local = grp * 64 + lane;
-    const int sp = wg_sp0 + sp_local;          // super-period of this lane
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int S = 64 / NT;                  // stream slots (SP runs) per track in a wave
+    const int lane = threadIdx.x;
+    const int tr = lane / S, spl = lane % S;    // compute mapping: lane = tr*S + spl
+    const int mix = blockIdx.x / a.tasks_per_mix;
+    const int task = blockIdx.x % a.tasks_per_mix;
+    const int s_first = (task * S + spl) * a.R;                 // this lane's first SP
+    char *slot = lds;
+    // the same slot as an LDS-space pointer: M0 for the DMA is then a plain
+    // constant (a generic->LDS cast would add a null check on SCC)
+    lds_char *slot3 = (lds_char *)(lds_void *)lds;
+    f2 *X = (f2 *)(lds + SLOT_BYTES);
 
-    const float *trk = a.in_ptrs ? (const float *)a.in_ptrs[(int64_t)mix * a.n_tracks + tr]
-                                 : a.in + (int64_t)mix * a.in_mix_stride + (int64_t)tr * a.in_track_stride;
-    // The resource starts 16 frames before the clip so every in-clip offset
-    // is non-negative (no 32-bit wrap): frame f lives at byte (f + 16) * 8 and
-    // num_records = (N + 16) * 8 makes every frame >= N read as 0.  The lane
-    // holding SP 0 sends its first 8 loads (frames -16..-1) out of range, so
-    // they read 0 too and the bytes before the clip are never touched.
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(trk + 2 * F0, (uint32_t)(a.frames_in - F0) * 8u);
-    const uint32_t vbase = (uint32_t)sp * (SPI * 8u);
-    const uint32_t vlo = sp == 0 ? 0x80000000u : vbase;
+    // one resource per mix, shifted 32 frames back so offsets stay >= 0
+    const float *mixbase = a.in + (int64_t)mix * a.in_mix_stride;
+    const uint32_t nrec = (uint32_t)((NT - 1) * a.track_bytes + ((int64_t)a.frames_in + 32) * 8);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(mixbase - 64, nrec);
 
+    // ---- DMA addressing (loader role): instruction d covers streams
+    // q = 4d..4d+3; lane l loads chunk j = ((l & 15) - q) & 15 of stream
+    // q = 4d + (l >> 4), which the hardware lands at slot + d*1024 + l*16.
+    // For S = 8 the byte offset splits into a wave-uniform part (soffset:
+    // track d/2, slot group 4*(d&1), segment, SP) and one of 4 per-lane
+    // parts (the chunk rotation depends on d only through d & 3).
+    static_assert(S == 8, "DMA address split assumes 8 stream slots per track");
+    const int lq = lane >> 4;                                   // stream within the 4 of an instruction
+    uint32_t vl[4];
+    int32_t fl[4];
+#pragma unroll
+    for (int d4 = 0; d4 < 4; ++d4) {
+        const int j = ((lane & 15) - lq - 4 * d4) & 15;
+        vl[d4] = (uint32_t)((task * S + lq) * a.R * (SPI * 8) + j * 16);
+        fl[d4] = (task * S + lq) * a.R * SPI - 32 + 2 * j;
+    }
+    const uint32_t TB = __builtin_amdgcn_readfirstlane((uint32_t)a.track_bytes);
+    const uint32_t GR = __builtin_amdgcn_readfirstlane((uint32_t)(4 * a.R * (SPI * 8)));   // slot group 4..7
+    const int N = a.frames_in;
+    // edge streams (clip start / end inside this task's span) need per-chunk redirects
+    const bool edge = __builtin_amdgcn_ballot_w64(s_first == 0 || (s_first + a.R) * SPI + 64 > N) != 0;
+
+    auto dma = [&](int r, int m) {   // segment m (0..6 rel to SP r) of every stream
+        // soffset = track part + slot-group part + SP + segment.  Built with a
+        // volatile s_add in place: left to itself LICM hoists all 112
+        // (instruction, segment) constants out of the SP loop and spills SGPRs.
+        const uint32_t rb0 = (uint32_t)(r * (SPI * 8) + m * 256);
+        const uint32_t rb1 = rb0 + GR;
+        if (!edge) {
+#pragma unroll
+            for (int d = 0; d < 16; ++d) {
+                uint32_t so;
+                asm volatile("s_mul_i32 %0, %1, %2\n\ts_add_u32 %0, %0, %3"
+                             : "=&s"(so) : "s"(TB), "n"(d >> 1), "s"((d & 1) ? rb1 : rb0) : "scc");
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(slot3 + d * 1024), 16, vl[d & 3], so, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < 16; ++d) {
+                uint32_t so;
+                asm volatile("s_mul_i32 %0, %1, %2\n\ts_add_u32 %0, %0, %3"
+                             : "=&s"(so) : "s"(TB), "n"(d >> 1), "s"((d & 1) ? rb1 : rb0) : "scc");
+                const int f = fl[d & 3] + 4 * (d & 1) * a.R * SPI + r * SPI + m * SEGF;
+                // out-of-clip chunks: push the whole offset past num_records
+                const uint32_t v = (f >= 0 && f + 1 < N) ? vl[d & 3] : OOB;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(slot3 + d * 1024), 16, v, so, 0, 0);
+            }
+        }
+    };
+    // ---- register window: rel frames [0, 224) of the current SP, one array
+    // per channel (kept scalar so nothing re-packs the VOP2 arithmetic)
+    float xl[WIN], xr[WIN];
+    auto copy_seg = [&](int m) {     // slot -> x[32m .. 32m+31] of this lane's stream
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // this wave's DMA landed
+        const char *base = slot + (lane >> 2) * 1024 + (lane & 3) * 256;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float4 v = *(const float4 *)(base + (((j + lane) & 15) * 16));
+            xl[SEGF * m + 2 * j] = v.x;
+            xr[SEGF * m + 2 * j] = v.y;
+            xl[SEGF * m + 2 * j + 1] = v.z;
+            xr[SEGF * m + 2 * j + 1] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // slot free for the next DMA
+    };
+
+    // ---- gain ramp of this lane's track
     XmhGain gp = a.g[0];
 #pragma unroll
     for (int i = 1; i < NT; ++i)
-        if (tr == i) gp = a.g[i];   // wave-uniform select: keeps the params in SGPRs
-    cfloat *Hk = (cfloat *)a.Hk;
+        if (tr == i) gp = a.g[i];
+    const bool xf = (gp.flags & XMH_GAIN_XFADE_OUT) != 0;
 
-    f2 x[2 * NPAIR];
-    auto load_pair = [&](int p) {
-        const float4 v = p < 8 ? bload(rs, vlo, p * 16) : bload(rs, vbase, p * 16);
-        x[2 * p] = f2{v.x, v.y};
-        x[2 * p + 1] = f2{v.z, v.w};
-    };
+    float *outb = a.out + (int64_t)mix * a.out_mix_stride;
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(outb, (uint32_t)a.frames_out * 8u);
+    cf2 *Hp = (cf2 *)a.Hk;   // [74][22] pairs (h_2i[t], h_2i+1[t])
 
-    // prologue: everything round 0 needs
-#pragma unroll
-    for (int p = first_pair(); p <= last_pair(G - 1); ++p) load_pair(p);
+    // prologue: segments 0, 1 of the first SP; segment 2 in flight
+    dma(0, 0);
+    copy_seg(0);
+    dma(0, 1);
+    copy_seg(1);
+    dma(0, 2);
 
-    float *ob = a.out_ptrs ? (float *)a.out_ptrs[mix] : a.out + (int64_t)mix * a.out_mix_stride;
-
-#pragma unroll
-    for (int q = 0; q < ROUNDS; ++q) {
-        const int k0 = q * G;
-        const int kend = k0 + G < SPO ? k0 + G : SPO;
-        // prefetch the pairs the next round adds
-        if (q + 1 < ROUNDS) {
-            const int kn = (q + 2) * G - 1 < SPO ? (q + 2) * G - 1 : SPO - 1;
-#pragma unroll
-            for (int p = last_pair(kend - 1) + 1; p <= last_pair(kn); ++p) load_pair(p);
-        }
-        // gains of this round (per lane: its SP's output frames n0..n0+7)
-        const int n0 = sp * SPO + k0;
-        float gk[G];
-        if (UNITY) {
-#pragma unroll
-            for (int i = 0; i < G; ++i) gk[i] = 1.0f;
-        } else {
-            const bool vary = gp.len == 0 ? (n0 < (int)gp.start && n0 + G - 1 >= (int)gp.start)
-                                          : (n0 + G - 1 > (int)gp.start && n0 < (int)gp.start + gp.len);
-            if (__builtin_amdgcn_ballot_w64(vary)) {
-#pragma unroll
-                for (int i = 0; i < G; ++i) gk[i] = gain_at(gp, n0 + i);
+#pragma unroll 1
+    for (int r = 0; r < a.R; ++r) {
+        const int s = s_first + r;
+        const int n_sp0 = s * SPO;
+        // gain class of this lane over the SP: 0 constant, 1 linear (inside the
+        // ramp, no clamp), 2 boundary (clamp or step inside the SP)
+        int cls;
+        float cA, cB = 0.0f, fkb = 0.0f;
+        {
+            const int st = (int)gp.start, ln = gp.len;
+            const int lo = n_sp0, hi = n_sp0 + SPO - 1;
+            const bool konst = ln == 0 ? !(lo < st && hi >= st) : (hi <= st || lo >= st + ln);
+            if (konst) {
+                cls = 0;
+                cA = gain_exact(gp, lo);
+            } else if (ln > 0 && lo >= st && hi <= st + ln) {
+                cls = 1;
+                cA = xf ? 1.0f : gp.g0;
+                cB = xf ? -gp.step : gp.step;
+                fkb = (float)(lo - st);
             } else {
-                const float g = gain_at(gp, n0);
-#pragma unroll
-                for (int i = 0; i < G; ++i) gk[i] = g;
+                cls = 2;
+                cA = 0.0f;
             }
         }
-        f2 *buf = xbuf + (q & 1) * (G * NT * SPWG);
-        // two outputs at a time: two independent add chains interleaved so the
-        // dependent pk_add latency of one hides behind the other's work
+        const bool any_lin = __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_ballot_w64(cls == 1) != 0));
+        const bool any_bnd = __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_ballot_w64(cls == 2) != 0));
+
 #pragma unroll
-        for (int k = k0; k < kend; k += 2) {
-            const bool two = k + 1 < kend;
-            cfloat *h0 = Hk + k * HK_STRIDE;
-            cfloat *h1 = Hk + (two ? k + 1 : k) * HK_STRIDE;
-            const int ra = rk(k), rb = rk(two ? k + 1 : k);
-            f2 acc0 = x[ra] * h0[0];
-            f2 acc1 = x[rb] * h1[0];
+        for (int q = 0; q < ROUNDS; ++q) {
+            const int k0 = q * G;
+            const int kend = k0 + G < SPO ? k0 + G : SPO;
+            float gk[G];
 #pragma unroll
-            for (int t = 1; t < TE; ++t) {
-                acc0 = acc0 + x[ra + t] * h0[t];
-                if (two) acc1 = acc1 + x[rb + t] * h1[t];
+            for (int i = 0; i < G; ++i) gk[i] = cA;
+            if (any_bnd) {
+#pragma unroll
+                for (int i = 0; i < G; ++i) gk[i] = gain_exact(gp, n_sp0 + k0 + i);
+            } else if (any_lin) {
+#pragma unroll
+                for (int i = 0; i < G; ++i) gk[i] = cA + cB * (fkb + (float)(k0 + i));
             }
-            buf[((k - k0) * NT + tr) * SPWG + sp_local] = UNITY ? acc0 : acc0 * gk[k - k0];
-            if (two) buf[((k + 1 - k0) * NT + tr) * SPWG + sp_local] = UNITY ? acc1 : acc1 * gk[k + 1 - k0];
+#pragma unroll
+            for (int k = k0; k < kend; k += 2) {
+                const bool two = k + 1 < kend;
+                // bring in the segments this pair needs (static schedule):
+                // copy segment m, then start the DMA of the next one
+#pragma unroll
+                for (int m = need_before(k) + 1; m <= need_pair(k); ++m) {
+                    copy_seg(m);
+                    if (m < 6) dma(r, m + 1);
+                    else if (r + 1 < a.R) dma(r + 1, 2);          // next SP's segment 2
+                }
+                // one s_load_dwordx2 pair (h_k[t], h_k+1[t]) feeds both outputs.
+                // Per-channel VOP2 v_mul_f32/v_add_f32 with a single-SGPR
+                // coefficient: the same VALU cycles as v_pk_* on the stereo
+                // pair (4 x 2 vs 2 x 4 per tap) but no SGPR-pair broadcasts,
+                // which the compiler otherwise materialises with s_mov and spills.
+                cf2 *hp = Hp + (k >> 1) * TE;
+                const int ra = rk(k), rb = rk(two ? k + 1 : k);
+                f2 h = hp[0];
+                float l0 = xl[ra] * h.x, r0 = xr[ra] * h.x;
+                float l1 = xl[rb] * h.y, r1 = xr[rb] * h.y;
+#pragma unroll
+                for (int t = 1; t < TE; ++t) {
+                    h = hp[t];
+                    l0 = l0 + xl[ra + t] * h.x;
+                    r0 = r0 + xr[ra + t] * h.x;
+                    if (two) {
+                        l1 = l1 + xl[rb + t] * h.y;
+                        r1 = r1 + xr[rb + t] * h.y;
+                    }
+                }
+                const f2 acc0 = f2{l0, r0}, acc1 = f2{l1, r1};
+                // exchange row kk: (track t, slot sp) at (t*S + sp + 4*kk) & 63
+                const int kk0 = k - k0, kk1 = k + 1 - k0;
+                X[kk0 * 64 + ((lane + 4 * kk0) & 63)] = acc0 * gk[kk0];
+                if (two) X[kk1 * 64 + ((lane + 4 * kk1) & 63)] = acc1 * gk[kk1];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // ordered track sum: lane' = (slot sp', output kk'), NT tracks each;
+            // 8 consecutive lanes store 8 consecutive frames (64 B) of one SP
+            {
+                constexpr int OPL = G * S / 64;            // outputs per lane (1 for NT = 8)
+#pragma unroll
+                for (int o = 0; o < OPL; ++o) {
+                    const int idx = o * 64 + lane;
+                    const int spo = idx / G, kk = idx % G;
+                    if (k0 + kk < kend) {
+                        f2 sum = X[kk * 64 + ((spo + 4 * kk) & 63)];
+#pragma unroll
+                        for (int t2 = 1; t2 < NT; ++t2) sum = sum + X[kk * 64 + ((t2 * S + spo + 4 * kk) & 63)];
+                        sum = sum + f2{0.0f, 0.0f};        // -0 -> +0 (scipy seeds are +0)
+                        const int64_t n = (int64_t)((task * S + spo) * a.R + r) * SPO + k0 + kk;
+                        if (n < a.frames_out)
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, sum), ro,
+                                                                  (uint32_t)n * 8u, 0, 0);
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        // LDS writes visible to the other waves; global loads stay in flight
-        // (a __syncthreads() fence would drain vmcnt, i.e. the prefetch).
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        // exchange: lane handles output k0 + kk of SP spo, summing NT tracks in order
-        constexpr int OUT_PER_LANE = (G * SPWG) / (64 * WAVES);   // = 8 / NT
+        // carry: the next SP's rel frames [21, 64) are this SP's [181, 224)
 #pragma unroll
-        for (int o = 0; o < OUT_PER_LANE; ++o) {
-            const int idx = (o * WAVES + w) * 64 + lane;          // 0 .. G*SPWG-1
-            const int kk = idx / SPWG, spo = idx % SPWG;
-            if (k0 + kk < kend) {
-                f2 s = buf[(kk * NT + 0) * SPWG + spo];
-#pragma unroll
-                for (int t2 = 1; t2 < NT; ++t2) s = s + buf[(kk * NT + t2) * SPWG + spo];
-                s = s + f2{0.0f, 0.0f};                           // -0 -> +0 (scipy seeds are +0)
-                const int64_t n = (int64_t)(wg_sp0 + spo) * SPO + k0 + kk;
-                if (n < a.frames_out) *(f2 *)(ob + n * 2) = s;
-            }
+        for (int f = CARRY0; f < 2 * SEGF; ++f) {
+            xl[f] = xl[f + SPI];
+            xr[f] = xr[f + SPI];
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outstanding at exit
 }
 
 }  // namespace
 
-// Host-side k-ordered coefficient table for the fast path:
-// Hk[k][t] = H[((k+rm)*M) % L][t], t < 22, rows padded to 24 floats.
-extern "C" int xmh_fast_table_147_160(const float *H, int T, float *Hk /* 147*24 */)
+// Host-side coefficient table for the fast path, pair-interleaved in output
+// order: Hp[i][t] = (H[ph(2i)][t], H[ph(2i+1)][t]), t < 22, ph(k) =
+// ((k+rm)*M) % L; the unpaired last output (k = 146) gets (h, 0).
+// 74 * 22 * 2 floats (13 KiB) — the table xm_table_build() uploads.
+extern "C" int xmh_fast_table_147_160(const float *H, int T, float *Hk /* >= 147*24 floats */)
 {
     if (T != 23) return -1003;
     for (int ph = 0; ph < L; ++ph)
         if (H[ph * T + 22] != 0.0f) return -1003;   // tap 22 must be an exact zero
-    for (int k = 0; k < SPO; ++k) {
-        const int ph = ((k + RM) * M) % L;
-        for (int t = 0; t < HK_STRIDE; ++t) Hk[k * HK_STRIDE + t] = t < TE ? H[ph * T + t] : 0.0f;
-    }
+    for (int i = 0; i < (SPO + 1) / 2; ++i)
+        for (int t = 0; t < TE; ++t) {
+            const int k0 = 2 * i, k1 = 2 * i + 1;
+            Hk[(i * TE + t) * 2 + 0] = H[(((k0 + RM) * M) % L) * T + t];
+            Hk[(i * TE + t) * 2 + 1] = k1 < SPO ? H[(((k1 + RM) * M) % L) * T + t] : 0.0f;
+        }
     return 0;
 }
 
 extern "C" int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_launches)
 {
     const int NT = j->n_tracks;
+    const int64_t N = j->frames_in;
     if (!(j->rs.L == L && j->rs.M == M && j->rs.rm == RM && j->rs.T == 23 && j->rs.Hrun) ||
-        j->fmt != 2 || j->channels != 2 || !(NT == 1 || NT == 2 || NT == 4 || NT == 8) ||
-        j->frames_in <= 0 || j->frames_in >= (1 << 27) || j->n_mix <= 0)
+        j->fmt != 2 || j->channels != 2 || NT != 8 || j->in_ptrs || j->out_ptrs || !j->gains_host ||
+        N <= 0 || (N & 1) || N >= (1 << 26) || j->n_mix <= 0)
         return -1003;   // not this kernel's job: generic path
+    const int64_t tb = j->in_track_stride * 4;
+    if (tb < N * 8 || (tb & 15) || ((uintptr_t)j->in & 15) || ((j->in_mix_stride * 4) & 15) ||
+        (NT - 1) * tb + (N + 32) * 8 >= ((int64_t)1 << 31))
+        return -1003;
     FastArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const float *)j->in;
-    a.in_track_stride = j->in_track_stride;
     a.in_mix_stride = j->in_mix_stride;
-    a.in_ptrs = j->in_ptrs;
+    a.track_bytes = tb;
     a.out = (float *)j->out;
     a.out_mix_stride = j->out_mix_stride;
-    a.out_ptrs = j->out_ptrs;
     a.Hk = j->rs.Hrun;
     a.n_mix = j->n_mix;
     a.n_tracks = NT;
-    a.frames_in = (int32_t)j->frames_in;
+    a.frames_in = (int32_t)N;
     a.frames_out = (int32_t)j->frames_out;
     a.n_sp = (int32_t)((j->frames_out + SPO - 1) / SPO);
-    const int spwg = 64 * (WAVES / NT);
-    a.groups_per_mix = (a.n_sp + spwg - 1) / spwg;
+    const int S = 64 / NT;
+    // SPs per lane: long runs amortise the per-task prologue; keep enough
+    // tasks to fill the 2048 wave slots (8 per CU) several times over
+    int R = 25;
+    while (R > 1 && (int64_t)a.n_mix * ((a.n_sp + S * R - 1) / (S * R)) < 4 * 2048) R = (R + 1) / 2;
+    a.R = R;
+    a.tasks_per_mix = (a.n_sp + S * R - 1) / (S * R);
     a.unity = j->unity;
-    if (!j->gains_host) return -1003;
     for (int i = 0; i < NT; ++i) {
         a.g[i] = j->gains_host[i];
-        // outputs are < 2^27: clamping the ramp start to +-2^28 keeps
-        // clamp(n - start, 0, len) unchanged and fits int32 arithmetic
-        const int64_t lim = (int64_t)1 << 28;
+        const int64_t lim = (int64_t)1 << 28;   // outputs < 2^26: keeps clamp(n-start) unchanged
         a.g[i].start = a.g[i].start < -lim ? -lim : (a.g[i].start > lim ? lim : a.g[i].start);
     }
-    const size_t lds = 2 * G * 512 * sizeof(f2);   // 64 KiB
-    const int64_t blocks = (int64_t)a.n_mix * a.groups_per_mix;
+    const size_t lds = LDS_PER_WAVE;
+    const int64_t blocks = (int64_t)a.n_mix * a.tasks_per_mix;
     if (blocks > 0x7fffffff) return -1003;
-    const bool u = j->unity && NT == 1;
-    auto kern = NT == 1 ? (u ? k_rs147_mix<1, true> : k_rs147_mix<1, false>)
-              : NT == 2 ? k_rs147_mix<2, false> : NT == 4 ? k_rs147_mix<4, false> : k_rs147_mix<8, false>;
-    static bool attr_done[5];
-    const int ai = NT == 1 ? (u ? 4 : 0) : NT == 2 ? 1 : NT == 4 ? 2 : 3;
-    if (!attr_done[ai]) {
+    auto kern = k_rs147_mix<8>;
+    static bool attr_done;
+    if (!attr_done) {
         if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return -1001;
-        attr_done[ai] = true;
+        attr_done = true;
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), lds, (hipStream_t)stream, a);
     if (n_launches) *n_launches += 1;
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
