@@ -1,31 +1,52 @@
 #!/usr/bin/env python3
-"""Time the headline kernel under XM_FAST_ABLATE variants, interleaved in one
-process (methodology: cdna_hip_programming.md §5.4 rule 24).  Profiling only."""
-import os, sys, json
+"""Performance attribution for the fast 147/160 kernel (dev tool, GPU box).
+
+Runs bench.py once per variant, each in its own process, and prints ms/step:
+  base        product library (lib/), inline-asm taps
+  ctaps       product library, compiler-scheduled taps (XM_FAST_TAPS=c)
+  abl<N>      lib_ablate/ build (`make ablate`), XM_FAST_ABLATE=N:
+              1 no DMA/copies, 2 no taps, 4 no exchange/track sum,
+              8 constant gains (combinations are sums)
+Ablated variants compute wrong results on purpose; only their time matters.
+usage: python tools/ablate.py [variant ...]
+"""
+import json
+import os
+import subprocess
+import sys
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "xm-audio-utils_amd"))
-import torch
-import xmaudio as xm
-sys.path.insert(0, ROOT)
-from bench import RAMPS, SEED
-B, ntr, N = int(os.environ.get("MIXES", 512)), 8, 480000
-m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
-m.set_tracks(RAMPS)
-F = m.out_frames(N)
-x = torch.empty((B, ntr, N, 2), dtype=torch.float32, device="cuda")
-y = torch.empty((B, F, 2), dtype=torch.float32, device="cuda")
-xm.synth(x.data_ptr(), "f32", SEED, 0, B * ntr, 2, N)
-s = torch.cuda.current_stream(); m.set_stream(s.cuda_stream)
-variants = [int(v) for v in (sys.argv[1:] or ["0", "1", "2", "4", "7"])]
-res = {v: [] for v in variants}
-for rnd in range(5):
-    for v in variants:
-        os.environ["XM_FAST_ABLATE"] = str(v)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)
-        e0.record(s)
-        for _ in range(3):
-            m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)
-        e1.record(s); torch.cuda.synchronize()
-        res[v].append(e0.elapsed_time(e1) / 3)
-print(json.dumps({v: [round(min(t), 3), round(sorted(t)[len(t)//2], 3)] for v, t in res.items()}))
+ABL_LIB = os.path.join(ROOT, "xm-audio-utils_amd", "lib_ablate", "libxm_audio.so")
+VARIANTS = {
+    "base": {},
+    "ctaps": {"XM_FAST_TAPS": "c"},
+}
+for n in (1, 2, 4, 8, 5, 6, 12, 13):
+    VARIANTS[f"abl{n}"] = {"XM_AUDIO_LIB": ABL_LIB, "XM_FAST_ABLATE": str(n)}
+
+
+def variant(name):
+    """name[@R]: a variant, optionally with the SPs-per-lane split forced to R"""
+    base, _, r = name.partition("@")
+    env = dict(VARIANTS[base])
+    if r:
+        env["XM_FAST_R"] = r
+    return env
+
+
+def main():
+    names = sys.argv[1:] or list(VARIANTS)
+    for name in names:
+        env = dict(os.environ, **variant(name))
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10", "--warmup", "2", "--no-cpu"]
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode or not line:
+            print(f"{name:8s} FAILED rc={p.returncode}: {p.stderr[-400:]}", flush=True)
+            break
+        d = json.loads(line[-1])
+        print(f"{name:8s} ms/step {d['ms_per_step']:8.4f}  kernel ms {d['roofline']['avg_launch_ms']:8.4f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -35,7 +35,8 @@ typedef struct XmhGain {
 typedef struct XmhResample {
     int32_t L, M, T, rm;      /* L == M == 1: no resampling */
     const float *H;           /* device, L*T floats (phase-major) */
-    const float *Hrun;        /* device, run-ordered table for the fast path (or NULL) */
+    int32_t fast;             /* 1: H equals the table baked into the 147/160 kernel */
+    int32_t pad;
 } XmhResample;
 
 /* ---------- one mix job (all pointers device) ------------------------------
@@ -105,9 +106,9 @@ const char *xmh_arch_name(void);
 /* resample (if rs.L != rs.M) + gain + ordered track sum; returns launches made */
 int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches);
 int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
-/* k-ordered coefficient table for the 147/160 fast kernel; -1003 if H does
- * not qualify (tap 22 of some phase non-zero) */
-int xmh_fast_table_147_160(const float *H, int T, float *Hk);
+/* 0 if the phase-major table H (L x T) equals, bit for bit, the coefficients
+ * baked into the 147/160 fast kernel (tools/gen_coefs.c); -1003 otherwise */
+int xmh_fast_table_check(const float *H, int L, int M, int T);
 /* synthetic PCM into device memory:
  * clip c of n_clips at out + c*frames*channels samples, id = clip0 + c. */
 int xmh_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,

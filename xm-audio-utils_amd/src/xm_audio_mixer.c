@@ -201,7 +201,7 @@ static void job_init(XmAudioMixer *m, XmhMixJob *j, size_t batch, size_t frames_
     j->rs.T = m->table.d.T;
     j->rs.rm = m->table.d.rm;
     j->rs.H = m->table.H_dev;
-    j->rs.Hrun = m->table.Hk_dev;
+    j->rs.fast = m->table.fast;
 }
 
 static int upload_gains(XmAudioMixer *m)
@@ -293,7 +293,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         x.rs.T = 1;
         x.rs.rm = 0;
         x.unity = 0;
-        x.rs.Hrun = NULL;
+        x.rs.fast = 0;
         rc = xmh_launch_mix(&x, m->stream, launches);
     }
     xmh_stream_sync(m->stream);

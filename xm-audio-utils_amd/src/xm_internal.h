@@ -18,7 +18,7 @@
 typedef struct XmTable {
     XmResampleDesign d;
     float *H_dev;          /* L*T floats on the handle's device */
-    float *Hk_dev;         /* 147/160 fast path: k-ordered [147][24] table, or NULL */
+    int fast;              /* 1: the baked 147/160 kernel computes exactly this table */
 } XmTable;
 
 int  xm_table_build(XmTable *t, int in_rate, int out_rate);

@@ -29,7 +29,8 @@ except ImportError:
     pass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libxm_audio.so")
+# XM_AUDIO_LIB: load another build of the same library (dev: ablation builds)
+LIB_PATH = os.environ.get("XM_AUDIO_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libxm_audio.so")
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"xmaudio: {LIB_PATH} is not built (run `make -C xm-audio-utils_amd`)")
 _lib = C.CDLL(LIB_PATH)
