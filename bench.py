@@ -41,7 +41,6 @@ for p in (os.path.join(ROOT, "xm-audio-utils_amd"), os.path.join(ROOT, "oracle")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 SEED = 0x584D4155
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -110,18 +109,14 @@ def cpu_baseline(args, ramps):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-
     import xmaudio as xm
+    from xmaudio import dist as xd
+
+    rk = xd.from_env()
+    world, rank = rk.world, rk.rank
+    torch.cuda.set_device(rk.local)
+    xd.init(rk, "nccl", torch.device("cuda", rk.local))   # RCCL; barrier + max-time only
+    dev = torch.cuda.current_device()
 
     B, ntr, N = args.mixes, args.tracks, args.frames
     ramps = RAMPS[:ntr] if ntr <= len(RAMPS) else (RAMPS * ((ntr + 7) // 8))[:ntr]
@@ -132,8 +127,8 @@ def main():
     x = torch.empty((B, ntr, N, 2), dtype=torch.float32, device="cuda")
     y = torch.empty((B, F, 2), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
-    # clip ids are global: rank r owns clips [r*B*ntr, (r+1)*B*ntr)
-    xm.synth(x.data_ptr(), "f32", SEED, rank * B * ntr, B * ntr, 2, N, dev, stream.cuda_stream)
+    # clip ids are global: rank r owns mixes [r*B, (r+1)*B) = clips [r*B*ntr, (r+1)*B*ntr)
+    xm.synth(x.data_ptr(), "f32", SEED, xd.first_clip(rk, B, ntr), B * ntr, 2, N, dev, stream.cuda_stream)
     mixer.set_stream(stream.cuda_stream)
     torch.cuda.synchronize()
 
@@ -147,8 +142,7 @@ def main():
 
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    xd.barrier(rk)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -156,15 +150,11 @@ def main():
         step()
         ev1[i].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    xd.barrier(rk)
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in zip(ev0, ev1)]
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = xd.max_over_ranks(rk, elapsed, device="cuda")
 
     ok = None
     if args.check and rank == 0:
@@ -203,9 +193,7 @@ def main():
         if ok is not None:
             line["parity_check_2mixes"] = ok
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    xd.finish(rk)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+LIB_DIR = os.path.join(ROOT, "xm-audio-utils_amd", "lib")
 for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "xm-audio-utils_amd"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)

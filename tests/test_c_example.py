@@ -1,0 +1,42 @@
+"""The drop-in boundary from C: examples/xm_mix_example.c compiles against
+include/*.h with plain gcc, links libxm_audio.so, and runs.  On a host without
+a GPU the library must refuse loudly (XM_EDEVICE, exit 2) instead of falling
+back to CPU; on the GPU box the example must complete (exit 0)."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import LIB_DIR, ROOT
+
+
+def _build(tmp_path):
+    exe = tmp_path / "xm_mix_example"
+    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "examples", "xm_mix_example.c"), "-L", LIB_DIR, "-lxm_audio",
+           f"-Wl,-rpath,{LIB_DIR}", "-lm", "-o", str(exe)]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_example_builds_and_refuses_without_gpu(tmp_path):
+    exe = _build(tmp_path)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    if "0 HIP device(s)" in p.stdout:
+        assert p.returncode == 2, p.stderr
+        assert "HIP device error" in p.stderr
+    else:   # a GPU is visible here: the full run must succeed
+        assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.gpu
+def test_example_runs_on_gpu(tmp_path):
+    exe = _build(tmp_path)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("mix ")]
+    assert len(lines) == 2
+    for ln in lines:
+        assert "44100 frames" in ln
+        rms = float(ln.rsplit("rms", 1)[1])
+        assert 0.05 < rms < 2.0
