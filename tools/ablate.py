@@ -5,8 +5,8 @@ Runs bench.py once per variant, each in its own process, and prints ms/step:
   base        product library (lib/), inline-asm taps
   ctaps       product library, compiler-scheduled taps (XM_FAST_TAPS=c)
   abl<N>      lib_ablate/ build (`make ablate`), XM_FAST_ABLATE=N:
-              1 no DMA/copies, 2 no taps, 4 no exchange/track sum,
-              8 constant gains (combinations are sums)
+              1 no DMA/copies, 2 no taps, 16 cycle attribution (17 = 1|16,
+              18 = 2|16); XM_FAST_TAPS=c|a selects the tap form
 Ablated variants compute wrong results on purpose; only their time matters.
 usage: python tools/ablate.py [variant ...]
 """
@@ -21,7 +21,7 @@ VARIANTS = {
     "base": {},
     "ctaps": {"XM_FAST_TAPS": "c"},
 }
-for n in (1, 2, 4, 8, 5, 6, 12, 13):
+for n in (1, 2, 16, 17, 18):
     VARIANTS[f"abl{n}"] = {"XM_AUDIO_LIB": ABL_LIB, "XM_FAST_ABLATE": str(n)}
 
 

@@ -26,8 +26,8 @@ xm.synth(x.data_ptr(), "f32", SEED, 0, B * NT, 2, N, 0, 0)
 lib = xm._lib
 f = lib.xm_dev_fast_prof
 f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-buf = (ctypes.c_ulonglong * 4)()
-for it in range(3):
+buf = (ctypes.c_ulonglong * 8)()
+for it in range(2):
     f(buf)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
@@ -35,7 +35,8 @@ for it in range(3):
     ev1.record()
     torch.cuda.synchronize()
     f(buf)
-    tot, wait, waves, pro = list(buf)
+    tot, wait, waves, issue, copy, ssum = list(buf)[:6]
     ms = ev0.elapsed_time(ev1)
     print(f"abl {os.environ['XM_FAST_ABLATE']} run {it}: {ms:.3f} ms  clock {tot / waves / (ms * 1e3):.0f} MHz(1 gen)  waves {waves}  cycles/wave {tot / waves:.0f}  "
-          f"dma-wait {100 * wait / tot:.1f}%  prologue {100 * pro / tot:.1f}%", flush=True)
+          f"dma-wait {100 * wait / tot:.1f}%  dma-issue {100 * issue / tot:.1f}%  "
+          f"copy {100 * copy / tot:.1f}%  sum-store {100 * ssum / tot:.1f}%", flush=True)

@@ -9,7 +9,7 @@ for f in sorted(glob.glob(os.path.join(d, "*", "run_kernel_stats.csv"))):
     for r in csv.DictReader(open(f)):
         print(f"trace  {r['Name'][:60]:60s} calls={r['Calls']} avg_ms={float(r['AverageNs'])/1e6:.4f}")
 agg = collections.defaultdict(list)
-for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         if pat in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))

@@ -45,6 +45,14 @@
 #include <type_traits>
 #include "xm_device.h"
 #include "xm_coefs_147_160.h"   // generated: kH147[147][22], XM_FAST_RM
+#include "xm_pk_taps.h"         // generated: packed-tap asm blocks (tools/gen_pk_asm.py)
+
+// cache policy of the once-read input stream (XM_DMA_NT=0 at build: default policy)
+#ifndef XM_DMA_NT_OFF
+#define XM_DMA_NT " nt"
+#else
+#define XM_DMA_NT ""
+#endif
 
 namespace {
 
@@ -68,6 +76,7 @@ constexpr int X_F2 = G * 64;               // exchange: 8 outputs x 64 lanes (f2
 constexpr int LDS_PER_WAVE = SLOT_BYTES + X_F2 * 8;   // 20 KiB
 constexpr int WAVES_PER_CU = 8;            // LDS-bound: 160 KiB / 20 KiB
 constexpr uint32_t OOB = 0x80000000u;      // offset beyond every num_records
+constexpr int DMA_PARTS = 8;               // a segment's 16 DMA instructions, 2 per output pair
 
 // rel frame (relative to 160*s - 32) of tap 0 of output k of SP s
 // (scipy: j0 = floor((m+rm)*M/L) - T + 1, T = 23)
@@ -104,13 +113,27 @@ struct Sched {
             if (k > lo && k < hi) ++n;
         return n;
     }
-    // vector-memory instructions issued after dma(m) and before copy_seg(m):
-    // only stores (one DMA segment is in flight at a time)
-    static constexpr int vm_after(int m)
+    // DMA of segment m is spread over DMA_PARTS pairs (2 instructions each),
+    // starting at the pair that copied segment m-1 (segment 2: at kc(6) of
+    // the previous SP, wrapping into the next SP's first pairs)
+    static constexpr int dma_start(int m) { return m == 2 ? kc(6) : kc(m - 1); }
+    // pair (in the copying SP's coordinates) of segment m's last DMA part
+    static constexpr int dma_last(int m) { return dma_start(m) + 2 * (DMA_PARTS - 1) - (m == 2 ? 2 * ((SPO + 1) / 2) : 0); }
+    // part of segment m's DMA issued at pair k of an SP (-1: none); for m == 2
+    // `next` selects the parts that belong to the following SP's segment 2
+    static constexpr int part_at(int k, int m, bool next)
     {
-        return m == 2 ? stores_in(kc(6), SPO) + stores_in(-1, kc(2)) : stores_in(kc(m - 1), kc(m));
+        if (m != 2) {
+            const int j = (k - dma_start(m)) / 2;
+            return k >= dma_start(m) && j < DMA_PARTS ? j : -1;
+        }
+        if (next) return k >= dma_start(2) ? (k - dma_start(2)) / 2 : -1;
+        const int j = (k + 2 * ((SPO + 1) / 2) - dma_start(2)) / 2;   // tail parts of this SP's own segment 2
+        return j < DMA_PARTS ? j : -1;
     }
-    static constexpr int prologue_pad() { return stores_in(kc(6), SPO); }
+    // vector-memory instructions issued after segment m's last DMA part and
+    // before copy_seg(m): only round stores (part windows never overlap)
+    static constexpr int vm_after(int m) { return stores_in(dma_last(m), kc(m)); }
 };
 
 struct FastArgs {
@@ -147,24 +170,42 @@ __device__ __forceinline__ float gain_exact(const XmhGain &g, int n)
     return (g.flags & XMH_GAIN_XFADE_OUT) ? 1.0f - v : v;
 }
 
+// the same coefficients pair-interleaved for the packed taps (TAPS == 2):
+// g_kHp[i][t] = (h_2i[t], h_2i+1[t]), read with scalar loads
+typedef const f2 __attribute__((address_space(4))) cf2;
+__constant__ float g_kHp[75][44] = XM_KHP147_INIT;   // + 1 zero row: prefetch past the end stays in bounds
+
+// coefficient groups of the packed taps: pair i = outputs (2i, 2i+1), group
+// g covers taps 8g .. min(8g+7, 21); 74 pairs x 3 groups per SP
+constexpr int CG_TAPS = 8;
+constexpr int CG_PER_PAIR = 3;
+__host__ __device__ constexpr int cg_ntaps(int g) { return g < 2 ? CG_TAPS : TE - 2 * CG_TAPS; }
+
 // coefficient bits as an integer (an "i" asm operand once k, t are unrolled)
 __device__ __forceinline__ constexpr int hbits(int k, int t) { return __builtin_bit_cast(int, kH147[k][t]); }
 
 #ifdef XM_FAST_ABLATION
 // per-launch cycle attribution (ABL & 16): [0] wave cycles, [1] cycles in
-// copy_seg's vmcnt waits, [2] waves, [3] cycles in the prologue
-__device__ unsigned long long g_fast_prof[4];
+// copy_seg's vmcnt waits, [2] waves, [3] cycles issuing DMA (incl. back-pressure),
+// [4] cycles from copy issue to data in VGPRs, [5] cycles in the track-sum store step
+__device__ unsigned long long g_fast_prof[8];
 #endif
 
 // ABL: ablation bits for performance attribution (dev builds only, see
 // `make ablate`; results are wrong by design): 1 no DMA/copies, 2 no taps,
 // 4 no exchange/track sum (a checksum is stored instead), 8 constant gains,
 // 16 cycle attribution into g_fast_prof (results stay exact).
-template <int NT, bool ASM, int ABL = 0>
+// TAPS: 0 compiler-scheduled VOP2 with literal coefficients, 1 the same as
+// opaque asm blocks, 2 packed v_pk_mul/v_pk_add on (L, R) with the
+// coefficient pair (h_k, h_k+1) in an SGPR pair selected by op_sel.
+template <int NT, int TAPS, int ABL = 0>
 __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     using SC = Sched<0>;
+    static_assert(SC::dma_last(2) < SC::kc(2) && SC::dma_last(3) < SC::kc(3) && SC::dma_last(4) < SC::kc(4) &&
+                      SC::dma_last(5) < SC::kc(5) && SC::dma_last(6) < SC::kc(6),
+                  "a segment's DMA parts must all be issued before its copy");
     constexpr int S = 64 / NT;                  // stream slots (SP runs) per track in a wave
     static_assert(S == 8, "DMA address split and exchange assume 8 tracks x 8 slots");
     const int lane = threadIdx.x;
@@ -205,18 +246,21 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
     const uint32_t GR = __builtin_amdgcn_readfirstlane((uint32_t)(4 * a.R * (SPI * 8)));   // slot group 4..7
     const int N = a.frames_in;
 
-    // segment m (0..6 relative to SP r) of every stream of the wave -> slot.
-    // s_waitcnt lgkmcnt(0) first: the previous copy's ds_reads of the slot
-    // must be done before the DMA can land on it.
-    auto dma = [&](int r, int m) {
+    // part j (instructions 2j, 2j+1) of segment m (0..6 relative to SP r) of
+    // every stream of the wave -> slot.  Part 0 waits lgkmcnt(0) first: the
+    // previous copy's ds_reads of the slot must be done before DMA lands on it.
+    uint64_t t_wait = 0, t_issue = 0, t_copy = 0, t_sum = 0;
+    auto dma_part = [&](int r, int m, int jp) {
         if (ABL & 1) return;
+        uint64_t ti0 = 0;
+        if (ABL & 16) ti0 = __builtin_amdgcn_s_memtime();
         const uint32_t rb0 = (uint32_t)(r * (SPI * 8) + m * 256);
         const uint32_t rb1 = rb0 + GR;
         // streams touching the clip start or end in this SP need per-chunk redirects
         const bool edge = __builtin_amdgcn_ballot_w64(s_first + r == 0 || (s_first + r + 1) * SPI + 32 > N) != 0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (jp == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int d = 0; d < 16; ++d) {
+        for (int d = 2 * jp; d < 2 * jp + 2; ++d) {
             uint32_t v = vl[d & 3];
             if (edge) {
                 const int f = fl[d & 3] + 4 * (d & 1) * a.R * SPI + r * SPI + m * SEGF;
@@ -227,36 +271,68 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
                          "s_add_u32 %0, %0, %3\n\t"
                          "s_add_u32 m0, %4, %5\n\t"
                          "s_nop 0\n\t"
-                         "buffer_load_dwordx4 %6, %7, %0 offen lds"
+                         "buffer_load_dwordx4 %6, %7, %0 offen" XM_DMA_NT " lds"
                          : "=&s"(so)
                          : "s"(TB), "n"(d >> 1), "s"((d & 1) ? rb1 : rb0), "s"(ldsb), "n"(d * 1024), "v"(v), "s"(rs)
                          : "memory", "scc", "m0");
         }
+        if (ABL & 16) t_issue += __builtin_amdgcn_s_memtime() - ti0;
+    };
+    auto dma = [&](int r, int m) {   // a whole segment at once (prologue)
+#pragma unroll
+        for (int jp = 0; jp < DMA_PARTS; ++jp) dma_part(r, m, jp);
     };
     // ---- register window: rel frames [0, 224) of the current SP, one array
     // per channel (kept scalar so nothing re-packs the VOP2 arithmetic)
-    uint64_t t_wait = 0;
     const uint64_t t_begin = (ABL & 16) ? __builtin_amdgcn_s_memtime() : 0;
-    float xl[WIN], xr[WIN];
+    float xl[WIN], xr[WIN];   // TAPS 0/1
+    f2 x2[WIN];               // TAPS 2: (L, R) in an aligned VGPR pair
     if (ABL & 1)
-        for (int f = 0; f < WIN; ++f) xl[f] = xr[f] = (float)(lane + f);
+#pragma unroll
+        for (int f = 0; f < WIN; ++f) {
+            if (TAPS == 2) x2[f] = f2{(float)(lane + f), (float)(lane - f)};
+            else xl[f] = xr[f] = (float)(lane + f);
+        }
+    float fake = 0.0f;   // ABL & 1: SP-dependent window contents, so nothing can be hoisted
     auto copy_seg = [&](int m, auto vm) {   // slot -> x[32m .. 32m+31] of this lane's stream
-        if (ABL & 1) return;
+        if (ABL & 1) {
+#pragma unroll
+            for (int j = 0; j < SEGF; ++j) {
+                if (TAPS == 2) {
+                    x2[SEGF * m + j] = f2{fake + (float)j, fake - (float)j};
+                } else {
+                    xl[SEGF * m + j] = fake + (float)j;
+                    xr[SEGF * m + j] = fake - (float)j;
+                }
+            }
+            return;
+        }
         uint64_t tw0 = 0;
         if (ABL & 16) tw0 = __builtin_amdgcn_s_memtime();
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(vm)::value) : "memory");   // dma(m) landed
+        uint64_t tw1 = 0;
         if (ABL & 16) {
+            tw1 = __builtin_amdgcn_s_memtime();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            t_wait += __builtin_amdgcn_s_memtime() - tw0;
+            t_wait += tw1 - tw0;
         }
         const char *base = slot + (lane >> 2) * 1024 + (lane & 3) * 256;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const float4 v = *(const float4 *)(base + (((j + lane) & 15) * 16));
-            xl[SEGF * m + 2 * j] = v.x;
-            xr[SEGF * m + 2 * j] = v.y;
-            xl[SEGF * m + 2 * j + 1] = v.z;
-            xr[SEGF * m + 2 * j + 1] = v.w;
+            if (TAPS == 2) {
+                x2[SEGF * m + 2 * j] = f2{v.x, v.y};
+                x2[SEGF * m + 2 * j + 1] = f2{v.z, v.w};
+            } else {
+                xl[SEGF * m + 2 * j] = v.x;
+                xr[SEGF * m + 2 * j] = v.y;
+                xl[SEGF * m + 2 * j + 1] = v.z;
+                xr[SEGF * m + 2 * j + 1] = v.w;
+            }
+        }
+        if (ABL & 16) {   // all 16 ds_read_b128 landed (serialises the copy: attribution only)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            t_copy += __builtin_amdgcn_s_memtime() - tw1;
         }
     };
 
@@ -281,6 +357,8 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
     };
     auto sum_store = [&](int rp, int qp, bool valid) {
         if (ABL & 4) return;
+        uint64_t ts0 = 0;
+        if (ABL & 16) ts0 = __builtin_amdgcn_s_memtime();
         f2 sum = pend[0];
 #pragma unroll
         for (int t2 = 1; t2 < NT; ++t2) sum = sum + pend[t2];
@@ -289,6 +367,24 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
         const int n = ((task * S + spo) * a.R + rp) * SPO + kq;   // >= frames_out: dropped by range check
         const uint32_t off = (valid && kq < SPO) ? (uint32_t)n * 8u : OOB;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, sum), ro, off, 0, 0);
+        if (ABL & 16) t_sum += __builtin_amdgcn_s_memtime() - ts0;
+    };
+
+    // ---- packed taps: the coefficient group in flight (8 SGPR pairs).  The
+    // loads are asm the compiler cannot see as pending, so every consumer sits
+    // behind an explicit lgkmcnt(0) (volatile asm keeps program order).
+    f2 cg[CG_TAPS];
+    const uint64_t hp_base = (uint64_t)(uintptr_t)&g_kHp[0][0];
+    auto cg_load = [&](int pi, int g) {
+        const uint32_t off = (uint32_t)(pi * 44 + g * 2 * CG_TAPS) * 4u;
+        asm volatile("s_load_dwordx2 %0, %8, %9\n\ts_load_dwordx2 %1, %8, %9 offset:8\n\t"
+                     "s_load_dwordx2 %2, %8, %9 offset:16\n\ts_load_dwordx2 %3, %8, %9 offset:24\n\t"
+                     "s_load_dwordx2 %4, %8, %9 offset:32\n\ts_load_dwordx2 %5, %8, %9 offset:40\n\t"
+                     "s_load_dwordx2 %6, %8, %9 offset:48\n\ts_load_dwordx2 %7, %8, %9 offset:56"
+                     : "=&s"(cg[0]), "=&s"(cg[1]), "=&s"(cg[2]), "=&s"(cg[3]), "=&s"(cg[4]), "=&s"(cg[5]),
+                       "=&s"(cg[6]), "=&s"(cg[7])
+                     : "s"(hp_base), "s"(off)
+                     : "memory");
     };
 
     // prologue: segments 0, 1 of the first SP in registers; segment 2 in
@@ -298,15 +394,16 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
     copy_seg(0, std::integral_constant<int, 0>{});
     dma(0, 1);
     copy_seg(1, std::integral_constant<int, 0>{});
-    dma(0, 2);
+    // segment 2's parts a previous SP would have issued; the first SP's own
+    // pairs issue the rest, so every copy_seg's vmcnt count is the steady one
 #pragma unroll
-    for (int i = 0; i < SC::prologue_pad(); ++i)
-        __builtin_amdgcn_raw_buffer_store_b64(v2u{0u, 0u}, ro, OOB, 0, 0);
+    for (int jp = 0; jp < DMA_PARTS; ++jp)
+        if (SC::part_at(SC::dma_start(2) + 2 * jp, 2, true) == jp && SC::dma_start(2) + 2 * jp < SPO) dma_part(0, 2, jp);
 
-    const uint64_t t_pro = (ABL & 16) ? __builtin_amdgcn_s_memtime() - t_begin : 0;
 #pragma unroll 1
     for (int r = 0; r < a.R; ++r) {
         const int s = s_first + r;
+        if (ABL & 1) fake = (float)(s * 3 + lane);
         const int n_sp0 = s * SPO;
         // gain class of this lane over the SP: 0 constant, 1 linear (inside the
         // ramp, no clamp), 2 boundary (clamp or step inside the SP)
@@ -329,6 +426,7 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
                 cA = 0.0f;
             }
         }
+        if (TAPS == 2) cg_load(0, 0);
         const bool any_lin = __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_ballot_w64(cls == 1) != 0));
         const bool any_bnd = __builtin_amdgcn_readfirstlane((int)(__builtin_amdgcn_ballot_w64(cls == 2) != 0));
 
@@ -364,37 +462,107 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
                 // independent mul/add chains (L, R of two outputs)
                 const int ra = rk(k), rb = rk(two ? k + 1 : k);
                 float l0, r0, l1 = 0.0f, r1 = 0.0f;
-                if (ASM) {
-                    // one opaque block per tap: 4 products into 4 temps, then
-                    // the 4 dependent adds (mul->add distance 4, see
-                    // tools/ubench/dep_latency.hip); coefficient bits inline
-                    if (two) {
-                        asm("v_mul_f32 %0, %4, %6\n\tv_mul_f32 %1, %4, %7\n\t"
-                            "v_mul_f32 %2, %5, %8\n\tv_mul_f32 %3, %5, %9"
-                            : "=&v"(l0), "=&v"(r0), "=&v"(l1), "=&v"(r1)
-                            : "i"(hbits(k, 0)), "i"(hbits(k + 1, 0)), "v"(xl[ra]), "v"(xr[ra]), "v"(xl[rb]), "v"(xr[rb]));
-                    } else {
-                        asm("v_mul_f32 %0, %2, %3\n\tv_mul_f32 %1, %2, %4"
-                            : "=&v"(l0), "=&v"(r0) : "i"(hbits(k, 0)), "v"(xl[ra]), "v"(xr[ra]));
-                    }
+                if (TAPS == 2 && !(ABL & 2)) {
+                    // (L, R) of outputs k and k+1; c = (h_k[t], h_k+1[t]) in
+                    // an SGPR pair: op_sel picks h_k for both halves of the
+                    // first product, h_k+1 for the second.  Per tap 2 pk_mul
+                    // + 2 pk_add instead of 4 + 4 VOP2.  Coefficients arrive
+                    // by explicit s_load one 8-tap group ahead (cg_load).
+                    const int pi = k >> 1;
+                    f2 a0, a1 = f2{0.0f, 0.0f};
+#define XM_X2(t) "v"(x2[ra + (t)]), "v"(x2[rb + (t)])
+#define XM_X1(t) "v"(x2[ra + (t)])
+#define XM_CUR "s"(cur[0]), "s"(cur[1]), "s"(cur[2]), "s"(cur[3]), "s"(cur[4]), "s"(cur[5]), "s"(cur[6]), "s"(cur[7])
 #pragma unroll
-                    for (int t = 1; t < TE; ++t) {
-                        float p0, p1, p2, p3;
-                        if (two) {
-                            asm("v_mul_f32 %0, %8, %10\n\tv_mul_f32 %1, %8, %11\n\t"
-                                "v_mul_f32 %2, %9, %12\n\tv_mul_f32 %3, %9, %13\n\t"
-                                "v_add_f32 %4, %4, %0\n\tv_add_f32 %5, %5, %1\n\t"
-                                "v_add_f32 %6, %6, %2\n\tv_add_f32 %7, %7, %3"
-                                : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "+v"(l0), "+v"(r0), "+v"(l1), "+v"(r1)
-                                : "i"(hbits(k, t)), "i"(hbits(k + 1, t)), "v"(xl[ra + t]), "v"(xr[ra + t]),
-                                  "v"(xl[rb + t]), "v"(xr[rb + t]));
-                        } else {
-                            asm("v_mul_f32 %0, %4, %5\n\tv_mul_f32 %1, %4, %6\n\t"
-                                "v_add_f32 %2, %2, %0\n\tv_add_f32 %3, %3, %1"
-                                : "=&v"(p0), "=&v"(p1), "+v"(l0), "+v"(r0)
-                                : "i"(hbits(k, t)), "v"(xl[ra + t]), "v"(xr[ra + t]));
-                        }
+                    for (int g = 0; g < CG_PER_PAIR; ++g) {
+                        // wait for this group, then prefetch the next one
+                        // (the next pair's first group; none past pair 73)
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        const f2 cur[CG_TAPS] = {cg[0], cg[1], cg[2], cg[3], cg[4], cg[5], cg[6], cg[7]};
+                        if (g + 1 < CG_PER_PAIR) cg_load(pi, g + 1);
+                        else if (pi + 1 < 74) cg_load(pi + 1, 0);
+                        f2 p0, p1, p2, p3;
+                        const int b = g * CG_TAPS;
+                        if (two && g == 0)
+                            asm volatile(XM_PK_G0_TWO
+                                         : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "=&v"(a0), "=&v"(a1)
+                                         : XM_CUR, XM_X2(0), XM_X2(1), XM_X2(2), XM_X2(3), XM_X2(4), XM_X2(5),
+                                           XM_X2(6), XM_X2(7));
+                        else if (two && g == 1)
+                            asm volatile(XM_PK_G1_TWO
+                                         : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "+v"(a0), "+v"(a1)
+                                         : XM_CUR, XM_X2(b + 0), XM_X2(b + 1), XM_X2(b + 2), XM_X2(b + 3),
+                                           XM_X2(b + 4), XM_X2(b + 5), XM_X2(b + 6), XM_X2(b + 7));
+                        else if (two)
+                            asm volatile(XM_PK_G2_TWO
+                                         : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "+v"(a0), "+v"(a1)
+                                         : XM_CUR, XM_X2(b + 0), XM_X2(b + 1), XM_X2(b + 2), XM_X2(b + 3),
+                                           XM_X2(b + 4), XM_X2(b + 5));
+                        else if (g == 0)
+                            asm volatile(XM_PK_G0_ONE
+                                         : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "=&v"(a0), "=&v"(a1)
+                                         : XM_CUR, XM_X1(0), XM_X1(1), XM_X1(2), XM_X1(3), XM_X1(4), XM_X1(5),
+                                           XM_X1(6), XM_X1(7));
+                        else if (g == 1)
+                            asm volatile(XM_PK_G1_ONE
+                                         : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "+v"(a0), "+v"(a1)
+                                         : XM_CUR, XM_X1(b + 0), XM_X1(b + 1), XM_X1(b + 2), XM_X1(b + 3),
+                                           XM_X1(b + 4), XM_X1(b + 5), XM_X1(b + 6), XM_X1(b + 7));
+                        else
+                            asm volatile(XM_PK_G2_ONE
+                                         : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "+v"(a0), "+v"(a1)
+                                         : XM_CUR, XM_X1(b + 0), XM_X1(b + 1), XM_X1(b + 2), XM_X1(b + 3),
+                                           XM_X1(b + 4), XM_X1(b + 5));
                     }
+#undef XM_X2
+#undef XM_X1
+#undef XM_CUR
+                    l0 = a0.x;
+                    r0 = a0.y;
+                    l1 = a1.x;
+                    r1 = a1.y;
+                } else if (TAPS == 2) {   // ABL & 2
+                    l0 = x2[ra].x;
+                    r0 = x2[ra].y;
+                    l1 = x2[rb].x;
+                    r1 = x2[rb].y;
+                } else if (TAPS == 1) {
+                    // VOP2 with literal coefficients, 4 taps per opaque block
+                    // (tools/gen_pk_asm.py): products of tap t+1 issue before
+                    // the adds of tap t; adds stay in tap order.
+#define XM_T2(t) "i"(hbits(k, t)), "i"(hbits(k + 1, t)), "v"(xl[ra + (t)]), "v"(xr[ra + (t)]), "v"(xl[rb + (t)]), "v"(xr[rb + (t)])
+#define XM_T1(t) "i"(hbits(k, t)), "v"(xl[ra + (t)]), "v"(xr[ra + (t)])
+                    float q0, q1, q2, q3, q4, q5, q6, q7;
+                    if (two) {
+                        asm volatile(XM_V2_F4_TWO
+                                     : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(q4), "=&v"(q5), "=&v"(q6),
+                                       "=&v"(q7), "=&v"(l0), "=&v"(r0), "=&v"(l1), "=&v"(r1)
+                                     : XM_T2(0), XM_T2(1), XM_T2(2), XM_T2(3));
+#pragma unroll
+                        for (int b = 4; b < 20; b += 4)
+                            asm volatile(XM_V2_R4_TWO
+                                         : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(q4), "=&v"(q5), "=&v"(q6),
+                                           "=&v"(q7), "+v"(l0), "+v"(r0), "+v"(l1), "+v"(r1)
+                                         : XM_T2(b), XM_T2(b + 1), XM_T2(b + 2), XM_T2(b + 3));
+                        asm volatile(XM_V2_R2_TWO
+                                     : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(q4), "=&v"(q5), "=&v"(q6),
+                                       "=&v"(q7), "+v"(l0), "+v"(r0), "+v"(l1), "+v"(r1)
+                                     : XM_T2(20), XM_T2(21));
+                    } else {
+                        asm volatile(XM_V2_F4_ONE
+                                     : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(l0), "=&v"(r0)
+                                     : XM_T1(0), XM_T1(1), XM_T1(2), XM_T1(3));
+#pragma unroll
+                        for (int b = 4; b < 20; b += 4)
+                            asm volatile(XM_V2_R4_ONE
+                                         : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "+v"(l0), "+v"(r0)
+                                         : XM_T1(b), XM_T1(b + 1), XM_T1(b + 2), XM_T1(b + 3));
+                        asm volatile(XM_V2_R2_ONE
+                                     : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "+v"(l0), "+v"(r0)
+                                     : XM_T1(20), XM_T1(21));
+                    }
+#undef XM_T2
+#undef XM_T1
                 } else if (ABL & 2) {
                     l0 = xl[ra];
                     r0 = xr[ra];
@@ -423,12 +591,14 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
                     if (q == 0) sum_store(r - 1, ROUNDS - 1, r > 0);
                     else sum_store(r, q - 1, true);
                 }
-                // 4. refill the slot behind each copy made above
+                // 4. refill the slot, 2 DMA instructions per pair: segments
+                // 3..6 of this SP, the tail of this SP's segment 2, and the
+                // head of the next SP's segment 2
 #pragma unroll
-                for (int m = SC::have_before(k) + 1; m <= SC::needc(k); ++m) {
-                    if (m < 6) dma(r, m + 1);
-                    else if (r + 1 < a.R) dma(r + 1, 2);          // next SP's segment 2
-                }
+                for (int m = 3; m <= 6; ++m)
+                    if (SC::part_at(k, m, false) >= 0) dma_part(r, m, SC::part_at(k, m, false));
+                if (SC::part_at(k, 2, false) >= 0) dma_part(r, 2, SC::part_at(k, 2, false));
+                if (SC::part_at(k, 2, true) >= 0 && r + 1 < a.R) dma_part(r + 1, 2, SC::part_at(k, 2, true));
                 // 5. exchange row kk: (track t, slot sp) at (t*S + sp + 4*kk) & 63
                 const int kk0 = k - k0, kk1 = k + 1 - k0;
                 if (ABL & 4) {
@@ -442,8 +612,12 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
         // carry: the next SP's rel frames [21, 64) are this SP's [181, 224)
 #pragma unroll
         for (int f = CARRY0; f < 2 * SEGF; ++f) {
-            xl[f] = xl[f + SPI];
-            xr[f] = xr[f + SPI];
+            if (TAPS == 2) {
+                x2[f] = x2[f + SPI];
+            } else {
+                xl[f] = xl[f + SPI];
+                xr[f] = xr[f + SPI];
+            }
         }
     }
     if (ABL & 4) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, chk), ro, (uint32_t)lane * 8u, 0, 0);
@@ -456,7 +630,9 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
         atomicAdd(&g_fast_prof[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_begin));
         atomicAdd(&g_fast_prof[1], (unsigned long long)t_wait);
         atomicAdd(&g_fast_prof[2], 1ull);
-        atomicAdd(&g_fast_prof[3], (unsigned long long)t_pro);
+        atomicAdd(&g_fast_prof[3], (unsigned long long)t_issue);
+        atomicAdd(&g_fast_prof[4], (unsigned long long)t_copy);
+        atomicAdd(&g_fast_prof[5], (unsigned long long)t_sum);
     }
 #endif
 }
@@ -465,11 +641,11 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
 
 #ifdef XM_FAST_ABLATION
 // dev builds: read and clear the cycle attribution counters
-extern "C" __attribute__((visibility("default"))) int xm_dev_fast_prof(unsigned long long *out4)
+extern "C" __attribute__((visibility("default"))) int xm_dev_fast_prof(unsigned long long *out8)
 {
-    static const unsigned long long zero[4] = {0, 0, 0, 0};
+    static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_fast_prof), sizeof zero) != hipSuccess ||
+        hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_fast_prof), sizeof zero) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(g_fast_prof), zero, sizeof zero) != hipSuccess)
         return -1001;
     return 0;
@@ -565,26 +741,21 @@ extern "C" int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_laun
     }
     const int64_t blocks = (int64_t)a.n_mix * a.tasks_per_mix;
     if (blocks > 0x7fffffff) return -1003;
-    const char *ab = getenv("XM_FAST_TAPS");   // "c": compiler-scheduled taps (A/B only)
-    const bool c_taps = ab && ab[0] == 'c';
-    auto kern = c_taps ? k_rs147_mix<8, false> : k_rs147_mix<8, true>;
+    // XM_FAST_TAPS (A/B only): "c" compiler-scheduled VOP2, "a" asm VOP2, default packed
+    const char *ab = getenv("XM_FAST_TAPS");
+    auto kern = k_rs147_mix<8, 2>;
+    if (ab && ab[0] == 'c') kern = k_rs147_mix<8, 0>;
+    if (ab && ab[0] == 'a') kern = k_rs147_mix<8, 1>;
 #ifdef XM_FAST_ABLATION
     const char *abl = getenv("XM_FAST_ABLATE");
+    const int tm = ab && ab[0] == 'c' ? 0 : (ab && ab[0] == 'a' ? 1 : 2);
+#define XM_ABL_CASE(n) \
+    case n: kern = tm == 0 ? k_rs147_mix<8, 0, n> : (tm == 1 ? k_rs147_mix<8, 1, n> : k_rs147_mix<8, 2, n>); break;
     switch (abl ? atoi(abl) : 0) {
-    case 1: kern = k_rs147_mix<8, false, 1>; break;
-    case 2: kern = k_rs147_mix<8, false, 2>; break;
-    case 4: kern = k_rs147_mix<8, false, 4>; break;
-    case 8: kern = k_rs147_mix<8, false, 8>; break;
-    case 5: kern = k_rs147_mix<8, false, 5>; break;
-    case 6: kern = k_rs147_mix<8, false, 6>; break;
-    case 12: kern = k_rs147_mix<8, false, 12>; break;
-    case 13: kern = k_rs147_mix<8, false, 13>; break;
-    case 16: kern = k_rs147_mix<8, false, 16>; break;
-    case 17: kern = k_rs147_mix<8, false, 17>; break;
-    case 18: kern = k_rs147_mix<8, false, 18>; break;
-    case 24: kern = k_rs147_mix<8, false, 24>; break;
+    XM_ABL_CASE(1) XM_ABL_CASE(2) XM_ABL_CASE(16) XM_ABL_CASE(17) XM_ABL_CASE(18)
     default: break;
     }
+#undef XM_ABL_CASE
 #endif
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), LDS_PER_WAVE, (hipStream_t)stream, a);
     if (n_launches) *n_launches += 1;

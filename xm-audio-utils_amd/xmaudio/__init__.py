@@ -199,10 +199,11 @@ class Mixer:
         self.channels = channels
         self.n_tracks = 1
 
-    def close(self):
+    # module globals may already be gone at interpreter exit: bind what close needs
+    def close(self, _vp=C.c_void_p, _byref=C.byref, _free=_lib.xm_audio_mixer_freep):
         if getattr(self, "_h", None):
-            h = C.c_void_p(self._h)
-            _lib.xm_audio_mixer_freep(C.byref(h))
+            h = _vp(self._h)
+            _free(_byref(h))
             self._h = None
 
     __del__ = close
@@ -265,10 +266,11 @@ class Effects:
             raise XmError(st.value, "xm_effects_create")
         self.channels = channels
 
-    def close(self):
+    # module globals may already be gone at interpreter exit: bind what close needs
+    def close(self, _vp=C.c_void_p, _byref=C.byref, _free=_lib.xm_effects_freep):
         if getattr(self, "_h", None):
-            h = C.c_void_p(self._h)
-            _lib.xm_effects_freep(C.byref(h))
+            h = _vp(self._h)
+            _free(_byref(h))
             self._h = None
 
     __del__ = close
