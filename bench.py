@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--cpu-mixes", type=int, default=48, help="mixes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--fill", choices=["synth", "zero", "tiny"], default="synth",
+                    help="dev only: input data (synth = the bench's synthetic PCM)")
     ap.add_argument("--check", action="store_true", help="bit-compare 2 mixes with the oracle after timing")
     return ap.parse_args()
 
@@ -134,6 +136,8 @@ def main():
     stream = torch.cuda.current_stream()
     # clip ids are global: rank r owns mixes [r*B, (r+1)*B) = clips [r*B*ntr, (r+1)*B*ntr)
     xm.synth(x.data_ptr(), "f32", SEED, xd.first_clip(rk, B, ntr), B * ntr, 2, N, dev, stream.cuda_stream)
+    if args.fill != "synth":   # dev: power/clock sensitivity to the data (not a bench line)
+        x.mul_(0.0 if args.fill == "zero" else 2.0 ** -20)
     mixer.set_stream(stream.cuda_stream)
     torch.cuda.synchronize()
 

@@ -286,3 +286,22 @@ def test_errors(xm, gpu):
     e2 = xm.Effects(48000, 2)
     with pytest.raises(xm.XmError):
         e2.add_biquad([1, 0, 0, 2, 0, 0])   # a0 != 1
+
+
+@pytest.mark.parametrize("n_sos", [1, 2, 5, 8, 15])
+@pytest.mark.parametrize("channels", [1, 2])
+def test_biquad_cascade_shapes(xm, gpu, n_sos, channels):
+    """Section-pipelined biquad kernel (lane = clip x section): every cascade
+    length up to XM_MAX_SOS, more clips than one wave holds, ragged lengths
+    around the 32-frame chunk, bit-compared with the C oracle (sosfilt order)."""
+    z = golden("effects.npz")
+    rng = np.random.default_rng(n_sos * 10 + channels)
+    sos = np.concatenate([z["sos"]] * 3)[:n_sos]
+    e = xm.Effects(48000, channels)
+    for s in sos:
+        e.add_biquad(s)
+    for B, N in [(1, 1), (3, 31), (2 * (64 // n_sos) + 1, 33), (17, 1000)]:
+        x = (rng.standard_normal((B, N, channels)) * 0.5).astype(np.float32)
+        y = e.process(x)
+        for b in range(B):
+            assert bits_equal(y[b], CO.biquad_f32(x[b], sos)), (B, N, b)

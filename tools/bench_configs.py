@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Secondary benchmarks: BASELINE.json configs 2-4 on one GPU (the per-GPU
+shard of each), one JSON line per config.  bench.py stays the headline.
+
+  python tools/bench_configs.py [c2 c3 c4 ...] [--steps K] [--warmup W]
+
+c2  48k->44.1k resample, 4096 stereo 10 s fp32 clips (1-track mixes, unity gain)
+c3  8-track s16 Q15 gain-ramp + crossfade mix, 1024 mixes x 10 s stereo 48 kHz
+c4  per-GPU shard of config 4: 1024 clips = 128 mixes x 8 tracks, resample ->
+    5-band RBJ EQ (biquad cascade) -> gain -> mix (8192 clips over 8 GPUs)
+Unit: input samples (frames x channels x tracks) per second; roofline
+fraction = algorithmic bytes (inputs once + output once) / kernel time / 8 TB/s.
+Inputs are synthetic PCM generated in HBM (xm_synth_pcm), outside the timing.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "xm-audio-utils_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import xmaudio as xm  # noqa: E402
+from bench import RAMPS, SEED, HBM_PEAK_GBS  # noqa: E402
+
+Q15_RAMPS = [dict(gain0_q15=29491), dict(gain0_q15=0, gain1_q15=26214, ramp_start=0, ramp_len=48000),
+             dict(gain0_q15=22938, gain1_q15=6554, ramp_start=240000, ramp_len=96000), dict(gain0_q15=16384),
+             dict(mode=1, ramp_start=144000, ramp_len=96000),
+             dict(gain0_q15=0, gain1_q15=32768, ramp_start=144000, ramp_len=96000),
+             dict(gain0_q15=32768, gain1_q15=0, ramp_start=432000, ramp_len=48000),
+             dict(gain0_q15=9830, gain1_q15=19661, ramp_start=300000, ramp_len=0)]
+EQ5 = [(xm.XM_EQ_LOWSHELF, 100.0, 3.0, 0.7), (xm.XM_EQ_PEAKING, 400.0, -2.0, 1.0),
+       (xm.XM_EQ_PEAKING, 1500.0, 2.5, 1.2), (xm.XM_EQ_PEAKING, 5000.0, -3.0, 0.9),
+       (xm.XM_EQ_HIGHSHELF, 10000.0, 4.0, 0.7)]
+
+
+def timed(step, steps, warmup, stream):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    return wall * 1e3, e0.elapsed_time(e1) / steps
+
+
+def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, **extra):
+    line = {"config": name, "workload": workload, "value": round(samples / (wall_ms * 1e-3) / 1e6, 1),
+            "unit": "Msamples/s", "ms_per_step": round(wall_ms, 4), "kernel_ms": round(ker_ms, 4),
+            "launches_per_step": mixer.timing().n_launches,
+            "roofline": {"bound": "hbm", "alg_bytes": alg_bytes,
+                         "achieved_GBps": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 1),
+                         "frac": round(alg_bytes / (ker_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+    line.update(extra)
+    print(json.dumps(line), flush=True)
+
+
+def c2(a):
+    B, N = a.clips, 480000
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    F = m.out_frames(N)
+    x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+    y = torch.empty((B, F, 2), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B, 2, N, 0, s.cuda_stream)
+    m.set_stream(s.cuda_stream)
+    w, k = timed(lambda: m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N), a.steps, a.warmup, s)
+    report("c2", f"48k->44.1k resample, {B} stereo 10 s fp32 clips", B * N * 2, B * N * 8 + B * F * 8, w, k, m)
+
+
+def c3(a):
+    B, ntr, N = a.mixes3, 8, 480000
+    m = xm.Mixer(48000, 48000, 2, "s16", mem="device")
+    m.set_tracks(Q15_RAMPS)
+    x = torch.empty((B, ntr, N, 2), dtype=torch.int16, device="cuda")
+    y = torch.empty((B, N, 2), dtype=torch.int16, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "s16", SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
+    m.set_stream(s.cuda_stream)
+    w, k = timed(lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), N * 2, B, N),
+                 a.steps, a.warmup, s)
+    report("c3", f"8-track s16 Q15 ramp/crossfade mix, {B} mixes x 10 s stereo 48 kHz", B * ntr * N * 2,
+           B * ntr * N * 4 + B * N * 4, w, k, m)
+
+
+def c4(a):
+    B, ntr, N = a.mixes4, 8, 480000
+    fx = xm.Effects(44100, 2, mem="device")
+    for band in EQ5:
+        fx.add_eq_band(*band)
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks(RAMPS)
+    m.set_track_effects(fx)
+    F = m.out_frames(N)
+    x = torch.empty((B, ntr, N, 2), dtype=torch.float32, device="cuda")
+    y = torch.empty((B, F, 2), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
+    m.set_stream(s.cuda_stream)
+    w, k = timed(lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N),
+                 a.steps, a.warmup, s)
+    report("c4", f"resample + 5-band EQ + 8-track mix, {B * ntr} clips per GPU (config 4 shard of 8192/8)",
+           B * ntr * N * 2, B * ntr * N * 8 + B * F * 8, w, k, m)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", nargs="*", default=["c2", "c3", "c4"])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--clips", type=int, default=4096)
+    ap.add_argument("--mixes3", type=int, default=1024)
+    ap.add_argument("--mixes4", type=int, default=128)
+    a = ap.parse_args()
+    for w in a.which:
+        globals()[w](a)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

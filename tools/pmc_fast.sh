@@ -1,19 +1,20 @@
 #!/bin/bash
-# PMC stall/issue counters for the headline kernel (dev; run on the GPU box
-# from the repo root).  Separate --pmc passes, never combined with tracing.
+# PMC issue/stall counters for the headline kernel (dev; run on the GPU box
+# from the repo root).  One --pmc pass per counter set, never combined with
+# tracing; each pass under its own time limit; stop at the first failure.
 #   tools/pmc_fast.sh <tag> [bench args...]
+# Extra environment (e.g. XM_AUDIO_LIB / XM_FAST_ABLATE) passes through.
 TAG=${1:-pmc}; shift
 ARGS=${@:---steps 3 --warmup 1 --no-cpu}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+export TMPDIR=/tmp
 i=0
 for set in \
-  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC" \
-  "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_LDS" \
-  "SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_IFETCH_LEVEL SQ_CYCLES" \
-  "SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_INSTS_SALU SQ_LEVEL_WAVES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE" ; do
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" \
+  "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA" \
+  "SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_IFETCH SQ_INSTS_BRANCH" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set -d $OUT/p$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || echo "pass $i failed rc=$?"
+  timeout -s KILL 120 rocprofv3 --pmc $set -d $OUT/p$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 tools/prof_summary.py $OUT

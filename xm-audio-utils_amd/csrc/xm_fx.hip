@@ -1,51 +1,134 @@
 // xm_fx.hip — effects chain kernels for gfx950 (biquad cascade, FIR) and the
 // synthetic PCM generator.
 //
-// Biquad: scipy sosfilt order (transposed DF-II, _signaltools.py:4601), one
-// lane per (clip, channel) stream, sections in order, state zero at clip
-// start.  The recurrence is serial in time, so exactness (SURVEY.md §7 hard
-// part 3) fixes the parallelism at clips x channels; coefficients live in
-// SGPRs (wave-uniform), state in VGPRs, input streamed with a 16-frame
-// register prefetch.
+// Biquad: scipy sosfilt order (transposed DF-II, _signaltools.py:4601),
+// sections in order, state zero at clip start.  The recurrence is serial in
+// time, so exactness (SURVEY.md §7 hard part 3) limits the parallelism to
+// clips x sections: k_biquad_lanes gives each (clip, section) its own lane
+// and chains the sections through LDS chunks (see the comment at the kernel).
 // FIR: upfirdn order (_upfirdn.py:107), taps staged in LDS, input tile in LDS.
+#include <stdlib.h>
 #include "xm_device.h"
 
 namespace {
 
-constexpr int BQ_THREADS = 64;
-constexpr int BQ_MAXSEC = 16;
+constexpr int BQ_MAXSEC = 15;   // XM_MAX_SOS (src/xm_internal.h): >= 4 clips per wave
 
+// Section-pipelined cascade.  The recurrence of one section is serial in
+// time, so the only parallelism that keeps sosfilt's rounding is across
+// clips and across sections: lane = (clip k, section s), lane = k*NS + s,
+// 64 / NS clips per wave (stereo (L, R) ride in one packed v_pk_* pair).
+// Time advances in chunks of CH frames; at step i lane s filters chunk i - s,
+// so the NS sections of a clip work on NS consecutive chunks at once and the
+// per-sample recurrence (4 dependent ops) is the only serial chain.
+//   section 0   reads its clip from HBM two chunks ahead into registers and
+//               passes the chunk through LDS like every other section;
+//   section s   reads the chunk lane - 1 (section s - 1) wrote one step earlier;
+//   last        stores to global memory instead of LDS.
+// One wave, so LDS needs no barrier: every read of a step precedes, in
+// program order, every write of that step.
+// In LDS a chunk is [CH / FPL][64 lanes][FPL frames] (16 B per lane-granule).
 template <int C>
-__global__ __launch_bounds__(BQ_THREADS) void k_biquad(XmhFxJob j)
+struct BqVec;
+template <>
+struct BqVec<1> { typedef float T; };
+template <>
+struct BqVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
+typedef float bq_f4 __attribute__((ext_vector_type(4)));
+
+template <int C, int CH>
+__global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
 {
-    const int stream = blockIdx.x * BQ_THREADS + threadIdx.x;
-    if (stream >= j.n_clips * C) return;
-    const int clip = stream / C, ch = stream % C;
-    const float *x = j.in_ptrs[clip];
-    float *y = j.out_ptrs[clip];
+    typedef typename BqVec<C>::T V;
+    typedef const __attribute__((address_space(1))) bq_f4 gcf4;
+    typedef __attribute__((address_space(1))) bq_f4 gf4;
+    constexpr int FPL = 4 / C;                     // frames per 16-B granule
+    constexpr int G = CH / FPL;                    // granules per chunk
+    __shared__ bq_f4 in_buf[G][64];                // section 0's input
+    __shared__ bq_f4 sec_buf[G][64];               // output of lane's section (s < NS - 1)
     const int ns = j.n_sos;
-    float z0[BQ_MAXSEC], z1[BQ_MAXSEC], q[BQ_MAXSEC][5];
-#pragma unroll
-    for (int s = 0; s < BQ_MAXSEC; ++s) {
-        z0[s] = 0.0f; z1[s] = 0.0f;
-        if (s < ns) {
-            q[s][0] = j.sos[6 * s + 0]; q[s][1] = j.sos[6 * s + 1]; q[s][2] = j.sos[6 * s + 2];
-            q[s][3] = j.sos[6 * s + 4]; q[s][4] = j.sos[6 * s + 5];
-        }
-    }
+    const int kpw = 64 / ns;                       // clips per wave
+    const int lane = threadIdx.x;
+    const int s = lane % ns, kk = lane / ns;
+    const int clip = blockIdx.x * kpw + kk;
+    const bool valid = kk < kpw && clip < j.n_clips;
+    const bool first = s == 0, last = s == ns - 1;
     const int64_t N = j.frames;
-    for (int64_t n = 0; n < N; ++n) {
-        float v = x[n * C + ch];
+    const int64_t nchunk = (N + CH - 1) / CH;
+    const float *x = valid ? j.in_ptrs[clip] : nullptr;
+    float *y = valid ? j.out_ptrs[clip] : nullptr;
+    const bq_f4 *src = first ? &in_buf[0][lane] : &sec_buf[0][(lane + 63) & 63];
+
+    const float *q = j.sos + 6 * s;                 // this lane's section, state zero at clip start
+    const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
+    V z0 = V(0.0f), z1 = V(0.0f);
+
+    bq_f4 pa[G], pb[G];                            // section 0: chunks i and i + 1 in flight
+    auto load = [&](bq_f4 (&d)[G], int64_t c) {
+        if (!(first && valid && c < nchunk) || (j.dev_flags & 1)) return;   // dev_flags 1: attribution, no loads
+        const float *xc = x + (size_t)C * (size_t)(c * CH);
+        if ((c + 1) * CH <= N && (((uintptr_t)xc) & 15) == 0) {
 #pragma unroll
-        for (int s = 0; s < BQ_MAXSEC; ++s) {
-            if (s < ns) {
-                const float o = q[s][0] * v + z0[s];
-                z0[s] = (q[s][1] * v - q[s][3] * o) + z1[s];
-                z1[s] = q[s][2] * v - q[s][4] * o;
-                v = o;
+            for (int g = 0; g < G; ++g) d[g] = ((gcf4 *)xc)[g];
+        } else {
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    d[g][e] = (c * CH + g * FPL) * C + e < N * C ? xc[g * 4 + e] : 0.0f;
+        }
+    };
+    auto step = [&](int64_t i, bq_f4 (&cur)[G]) {
+        if (first) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) in_buf[g][lane] = cur[g];
+        }
+        load(cur, i + 2);                          // refill: chunk i + 2
+        const int64_t c = i - s;                   // chunk this lane filters
+        bq_f4 v4[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) v4[g] = src[g * 64];
+        if (c >= 0 && c < nchunk) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                bq_f4 r;
+#pragma unroll
+                for (int e = 0; e < FPL; ++e) {
+                    V v;
+                    if constexpr (C == 2) v = V{v4[g][2 * e], v4[g][2 * e + 1]};
+                    else v = v4[g][e];
+                    const V o = b0 * v + z0;              // sosfilt (_sosfilt.pyx) order
+                    z0 = (b1 * v - a1 * o) + z1;
+                    z1 = b2 * v - a2 * o;
+                    if constexpr (C == 2) { r[2 * e] = o.x; r[2 * e + 1] = o.y; }
+                    else r[e] = o;
+                }
+                v4[g] = r;
+            }
+            if (!last) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) sec_buf[g][lane] = v4[g];
+            } else if (valid) {
+                float *yc = y + (size_t)C * (size_t)(c * CH);
+                if ((c + 1) * CH <= N && (((uintptr_t)yc) & 15) == 0) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) ((gf4 *)yc)[g] = v4[g];
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if ((c * CH + g * FPL) * C + e < N * C) yc[g * 4 + e] = v4[g][e];
+                }
             }
         }
-        y[n * C + ch] = v;
+    };
+    load(pa, 0);
+    load(pb, 1);
+    const int64_t steps = nchunk + ns - 1;
+    for (int64_t i = 0; i < steps; i += 2) {
+        step(i, pa);
+        if (i + 1 < steps) step(i + 1, pb);
     }
 }
 
@@ -126,11 +209,14 @@ __global__ __launch_bounds__(256) void k_synth(void *out, int fmt, uint64_t seed
 
 extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
 {
-    if (j->n_sos > BQ_MAXSEC) return -1003;
-    const int streams = j->n_clips * j->channels;
-    dim3 grid((streams + BQ_THREADS - 1) / BQ_THREADS);
-    if (j->channels == 1) hipLaunchKernelGGL(k_biquad<1>, grid, BQ_THREADS, 0, (hipStream_t)stream, *j);
-    else hipLaunchKernelGGL(k_biquad<2>, grid, BQ_THREADS, 0, (hipStream_t)stream, *j);
+    if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
+    if (j->n_clips == 0 || j->frames == 0) return 0;
+    const int kpw = 64 / j->n_sos;
+    dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
+    auto kern = j->channels == 1 ? k_biquad_lanes<1, 32> : k_biquad_lanes<2, 32>;
+    XmhFxJob jj = *j;
+    if (const char *d = getenv("XM_FX_DEV")) jj.dev_flags = atoi(d);   // dev attribution knob
+    hipLaunchKernelGGL(kern, grid, dim3(64), 0, (hipStream_t)stream, jj);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
 

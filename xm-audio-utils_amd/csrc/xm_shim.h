@@ -79,6 +79,8 @@ typedef struct XmhFxJob {
     int32_t n_sos;
     int32_t fir_len;
     const float *fir;              /* device fir_len taps */
+    int32_t dev_flags;             /* dev/attribution only (XM_FX_DEV env), 0 in the product */
+    int32_t reserved;
 } XmhFxJob;
 
 /* ---------- runtime --------------------------------------------------------- */

@@ -10,7 +10,7 @@
 #include "../csrc/xm_shim.h"
 
 #define XM_MAX_TRACKS 64
-#define XM_MAX_SOS 16
+#define XM_MAX_SOS 15   /* one wave per section + a loader wave <= 1024 threads (csrc/xm_fx.hip) */
 #define XM_MAX_FIR 4096
 #define XM_MAX_EFFECTS 32
 
