@@ -305,3 +305,16 @@ def test_biquad_cascade_shapes(xm, gpu, n_sos, channels):
         y = e.process(x)
         for b in range(B):
             assert bits_equal(y[b], CO.biquad_f32(x[b], sos)), (B, N, b)
+
+
+@pytest.mark.parametrize("B,N", [(8, 4800), (9, 48000), (17, 9602), (3, 4800), (16, 480000)])
+def test_resample_only_batches(xm, gpu, B, N):
+    """Config 2 shape: 1-track unity-gain resampling of a batch of clips (the
+    fast kernel's split mode takes 8 clips per pseudo-mix, the remainder and
+    batches under 8 run the generic kernel); every clip bit-compared."""
+    x = np.stack([O.gen_f32(SEED, 3100 + b, 2, N) for b in range(B)])[:, None]
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    y = m.process(x)
+    idx = range(B) if N < 100000 else (0, 7, 8, 15)
+    for b in idx:
+        assert bits_equal(y[b], CO.resample_f32(x[b, 0], 147, 160)), b

@@ -96,7 +96,7 @@ static_assert(last_seg(0) == 1, "first outputs need segments 0,1");
 //   DMA of the segment after each one copied here
 //   exchange writes of outputs k, k+1
 // E = how many segments ahead of need a segment is copied into registers.
-template <int E>
+template <int E, int NSTORE = 1>   // NSTORE: vector stores per store event
 struct Sched {
     static constexpr int needc(int k) { return need_pair(k) + E > 6 ? 6 : need_pair(k) + E; }
     static constexpr int have_before(int k) { return k == 0 ? 1 : needc(k - 2); }
@@ -133,7 +133,7 @@ struct Sched {
     }
     // vector-memory instructions issued after segment m's last DMA part and
     // before copy_seg(m): only round stores (part windows never overlap)
-    static constexpr int vm_after(int m) { return stores_in(dma_last(m), kc(m)); }
+    static constexpr int vm_after(int m) { return NSTORE * stores_in(dma_last(m), kc(m)); }
 };
 
 struct FastArgs {
@@ -148,6 +148,7 @@ struct FastArgs {
     int32_t R;                       // SPs per lane (consecutive)
     int32_t tasks_per_mix;
     int32_t unity;
+    int64_t out_clip_stride;         // SPLIT: floats between the 8 clips' outputs
     XmhGain g[8];
 };
 
@@ -198,11 +199,16 @@ __device__ unsigned long long g_fast_prof[8];
 // TAPS: 0 compiler-scheduled VOP2 with literal coefficients, 1 the same as
 // opaque asm blocks, 2 packed v_pk_mul/v_pk_add on (L, R) with the
 // coefficient pair (h_k, h_k+1) in an SGPR pair selected by op_sel.
-template <int NT, int TAPS, int ABL = 0>
+// SPLIT: resample only (config 2) — the 8 "tracks" are 8 independent clips
+// at unity gain and each is stored to its own output instead of being summed
+// (out = r + 0, the contract's 1-track mix).
+template <int NT, int TAPS, int ABL = 0, bool SPLIT = false>
 __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    using SC = Sched<0>;
+    using SC = Sched<0, SPLIT ? NT : 1>;
+    static_assert(SC::vm_after(2) < 64 && SC::vm_after(3) < 64 && SC::vm_after(4) < 64 && SC::vm_after(5) < 64 &&
+                      SC::vm_after(6) < 64, "vmcnt is 6 bits");
     static_assert(SC::dma_last(2) < SC::kc(2) && SC::dma_last(3) < SC::kc(3) && SC::dma_last(4) < SC::kc(4) &&
                       SC::dma_last(5) < SC::kc(5) && SC::dma_last(6) < SC::kc(6),
                   "a segment's DMA parts must all be issued before its copy");
@@ -344,7 +350,8 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
     const bool xf = (gp.flags & XMH_GAIN_XFADE_OUT) != 0;
 
     float *outb = a.out + (int64_t)mix * a.out_mix_stride;
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc(outb, (uint32_t)a.frames_out * 8u);
+    const uint32_t clip_bytes = SPLIT ? (uint32_t)a.out_clip_stride * 4u : 0u;
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(outb, (NT - 1) * clip_bytes + (uint32_t)a.frames_out * 8u);
 
     // ---- track-sum role: lane' = (slot spo, output kk of the round)
     const int spo = lane / G, kkp = lane % G;
@@ -359,14 +366,26 @@ __global__ __launch_bounds__(64) void k_rs147_mix(FastArgs a)
         if (ABL & 4) return;
         uint64_t ts0 = 0;
         if (ABL & 16) ts0 = __builtin_amdgcn_s_memtime();
-        f2 sum = pend[0];
-#pragma unroll
-        for (int t2 = 1; t2 < NT; ++t2) sum = sum + pend[t2];
-        sum = sum + f2{0.0f, 0.0f};              // -0 -> +0 (scipy seeds are +0)
         const int kq = qp * G + kkp;
         const int n = ((task * S + spo) * a.R + rp) * SPO + kq;   // >= frames_out: dropped by range check
-        const uint32_t off = (valid && kq < SPO) ? (uint32_t)n * 8u : OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, sum), ro, off, 0, 0);
+        if constexpr (SPLIT) {
+            // one store per clip, every one issued (vmcnt accounting); n past
+            // the clip end would land in the next clip: send it out of range
+            const bool ok = valid && kq < SPO && n < a.frames_out;
+#pragma unroll
+            for (int t2 = 0; t2 < NT; ++t2) {
+                const f2 v = pend[t2] + f2{0.0f, 0.0f};   // -0 -> +0 (scipy seeds are +0)
+                const uint32_t off = ok ? (uint32_t)t2 * clip_bytes + (uint32_t)n * 8u : OOB;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), ro, off, 0, 0);
+            }
+        } else {
+            f2 sum = pend[0];
+#pragma unroll
+            for (int t2 = 1; t2 < NT; ++t2) sum = sum + pend[t2];
+            sum = sum + f2{0.0f, 0.0f};              // -0 -> +0 (scipy seeds are +0)
+            const uint32_t off = (valid && kq < SPO) ? (uint32_t)n * 8u : OOB;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, sum), ro, off, 0, 0);
+        }
         if (ABL & 16) t_sum += __builtin_amdgcn_s_memtime() - ts0;
     };
 
@@ -700,31 +719,41 @@ static void pick_split(int64_t n_mix, int n_sp, int S, int *R_out, int *tpm_out)
     *tpm_out = bestT;
 }
 
+extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_launches);
+
 extern "C" int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_launches)
 {
     const int NT = j->n_tracks;
     const int64_t N = j->frames_in;
     if (!(j->rs.L == L && j->rs.M == M && j->rs.rm == RM && j->rs.T == 23 && j->rs.fast) ||
-        j->fmt != 2 || j->channels != 2 || NT != 8 || j->in_ptrs || j->out_ptrs || !j->gains_host ||
+        j->fmt != 2 || j->channels != 2 || j->in_ptrs || j->out_ptrs || !j->gains_host ||
         N <= 0 || (N & 1) || N >= (1 << 26) || j->n_mix <= 0)
         return -1003;   // not this kernel's job: generic path
-    const int64_t tb = j->in_track_stride * 4;
-    if (tb < N * 8 || (tb & 15) || ((uintptr_t)j->in & 15) || ((j->in_mix_stride * 4) & 15) ||
-        (NT - 1) * tb + (N + 32) * 8 >= ((int64_t)1 << 31))
+    // 8-track mixes, or (split) 1-track unity-gain resampling of >= 8 clips,
+    // taken 8 clips at a time as the 8 "tracks" of a pseudo-mix
+    const bool split = NT == 1 && j->unity && j->n_mix >= 8;
+    if (NT != 8 && !split) return -1003;
+    const int64_t tb = split ? j->in_mix_stride * 4 : j->in_track_stride * 4;
+    const int64_t in_mix = split ? 8 * j->in_mix_stride : j->in_mix_stride;
+    if (tb < N * 8 || (tb & 15) || ((uintptr_t)j->in & 15) || ((in_mix * 4) & 15) ||
+        7 * tb + (N + 32) * 8 >= ((int64_t)1 << 31))
+        return -1003;
+    if (split && (j->out_mix_stride < j->frames_out * 2 || 7 * j->out_mix_stride * 4 + j->frames_out * 8 >= ((int64_t)1 << 31)))
         return -1003;
     FastArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const float *)j->in;
-    a.in_mix_stride = j->in_mix_stride;
+    a.in_mix_stride = in_mix;
     a.track_bytes = tb;
     a.out = (float *)j->out;
-    a.out_mix_stride = j->out_mix_stride;
-    a.n_mix = j->n_mix;
-    a.n_tracks = NT;
+    a.out_mix_stride = split ? 8 * j->out_mix_stride : j->out_mix_stride;
+    a.out_clip_stride = split ? j->out_mix_stride : 0;
+    a.n_mix = split ? j->n_mix / 8 : j->n_mix;
+    a.n_tracks = 8;
     a.frames_in = (int32_t)N;
     a.frames_out = (int32_t)j->frames_out;
     a.n_sp = (int32_t)((j->frames_out + SPO - 1) / SPO);
-    const int S = 64 / NT;
+    const int S = 64 / 8;
     pick_split(a.n_mix, a.n_sp, S, &a.R, &a.tasks_per_mix);
     if (const char *fr = getenv("XM_FAST_R")) {   // dev knob: force SPs per lane
         const int R = atoi(fr);
@@ -734,7 +763,12 @@ extern "C" int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_laun
         }
     }
     a.unity = j->unity;
-    for (int i = 0; i < NT; ++i) {
+    for (int i = 0; i < 8; ++i) {
+        if (split) {
+            memset(&a.g[i], 0, sizeof a.g[i]);
+            a.g[i].g0 = a.g[i].g1 = 1.0f;
+            continue;
+        }
         a.g[i] = j->gains_host[i];
         const int64_t lim = (int64_t)1 << 28;   // outputs < 2^26: keeps clamp(n-start) unchanged
         a.g[i].start = a.g[i].start < -lim ? -lim : (a.g[i].start > lim ? lim : a.g[i].start);
@@ -757,7 +791,17 @@ extern "C" int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_laun
     }
 #undef XM_ABL_CASE
 #endif
+    if (split) kern = k_rs147_mix<8, 2, 0, true>;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), LDS_PER_WAVE, (hipStream_t)stream, a);
     if (n_launches) *n_launches += 1;
-    return hipGetLastError() == hipSuccess ? 0 : -1001;
+    if (hipGetLastError() != hipSuccess) return -1001;
+    if (split && j->n_mix % 8) {   // the last n_mix % 8 clips: generic kernel
+        XmhMixJob r = *j;
+        const int64_t done = (int64_t)a.n_mix * 8;
+        r.n_mix = (int32_t)(j->n_mix - done);
+        r.in = (const float *)j->in + done * j->in_mix_stride;
+        r.out = (float *)j->out + done * j->out_mix_stride;
+        return xmh_launch_mix_generic(&r, stream, n_launches);
+    }
+    return 0;
 }
