@@ -96,6 +96,31 @@ XM_API int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in,
                                    void *out, ptrdiff_t out_mix_stride,
                                    size_t batch, size_t frames_in);
 
+/* ---- cross-device mixdown (BASELINE.json:11, config 5: the tracks of one mix
+ * live on different devices).  Each device runs the tracks it holds through
+ * process_partial_s16, which writes the Q15 track sum of every output sample
+ * as int32 WITHOUT the final saturation.  The caller adds the partials of all
+ * devices (any order and grouping: <= 64 tracks of |term| <= 65535 cannot
+ * overflow int32, so the sum is exact, e.g. an RCCL reduce-scatter over
+ * xGMI), and finish_s16 saturates.  partial + exchange + finish equals
+ * process_* over all the tracks, bit for bit.  Gains are evaluated at the
+ * mix's output frame index, so a device holding tracks [t0, t1) simply sets
+ * those tracks' ramps.  S16 mixers with XM_MEM_DEVICE only (else XM_ENOSYS);
+ * no per-track effects.  Layouts as process_strided (strides in elements);
+ * partial + b*partial_mix_stride holds out_frames*channels int32. */
+XM_API int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in,
+                                       ptrdiff_t in_track_stride, ptrdiff_t in_mix_stride,
+                                       int32_t *partial, ptrdiff_t partial_mix_stride,
+                                       size_t batch, size_t frames_in);
+
+/* out + b*out_mix_stride gets saturate16(sum over p < n_parts, in p order, of
+ * partials[p*part_stride + b*partial_mix_stride + i]) for every sample
+ * i < out_frames*channels.  n_parts in [1, 64]; strides in elements. */
+XM_API int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, int n_parts,
+                              ptrdiff_t part_stride, ptrdiff_t partial_mix_stride,
+                              int16_t *out, ptrdiff_t out_mix_stride,
+                              size_t batch, size_t out_frames);
+
 XM_API int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t);
 
 /* Destroy and NULL the handle (no-op on NULL). */

@@ -79,3 +79,69 @@ def test_two_rank_shards_union_equals_single_process():
     for rank, gathered, slowest in res:
         assert slowest == float(world)                       # max over ranks
         assert sum(gathered, []) == want                     # rank r owns mixes [2r, 2r+2)
+
+
+# ---- config 5 (BASELINE.json:11): tracks of every mix spread over the ranks
+B5, NT5, F5 = 4, 16, 3001
+RAMPS5 = [dict(gain0_q15=q, gain1_q15=q2, ramp_start=s, ramp_len=ln, mode=md)
+          for q, q2, s, ln, md in [(32768, 32768, 0, 0, 0), (0, 32768, 100, 2000, 0), (65535, 100, 0, 3001, 0),
+                                   (16384, 16384, 0, 0, 0), (0, 0, 500, 900, 1), (0, 32768, 500, 900, 0),
+                                   (40000, 3, 2000, 13, 0), (7, 60000, 1500, 0, 0)] * 2]
+
+
+def _tracks5(b):
+    import np_oracle as O
+    from bench import SEED
+    tr = [O.gen_s16(SEED, 64 * b + t, 2, F5) for t in range(NT5)]
+    for t in range(4):              # loud tracks: the 16-track sum saturates
+        tr[t][50:150] = 32767
+    return tr
+
+
+def _worker5(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (os.path.join(ROOT, "xm-audio-utils_amd"), os.path.join(ROOT, "oracle"), ROOT):
+        sys.path.insert(0, p)
+    import torch
+    import np_oracle as O
+    from xmaudio import dist as xd
+
+    rk = xd.from_env()
+    xd.init(rk, "gloo")
+    per = NT5 // world
+    mine = range(per * rank, per * (rank + 1))        # this rank's tracks of every mix
+    part = np.stack([O.mix_s16_partial([_tracks5(b)[t] for t in mine], [RAMPS5[t] for t in mine]).reshape(-1)
+                     for b in range(B5)])
+    blk = xd.reduce_partials(rk, torch.from_numpy(part))
+    first, n = xd.owned_mixes(rk, B5)
+    y = O.sat16(blk.numpy().astype(np.int64)).reshape(n, F5, 2)
+    xd.finish(rk)
+    q.put((rank, first, y))
+
+
+def test_two_rank_spanning_mixdown_equals_full_mix():
+    """Config 5 exchange on CPU: each rank holds half of the 16 tracks of every
+    mix, forms the int32 Q15 partial, the partials meet in reduce_partials
+    (RCCL reduce-scatter on GPUs; all-reduce + block on gloo) and the owner
+    saturates: every mix equals the one-process 16-track mix bit for bit."""
+    import np_oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker5, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = {}
+    for rank, first, y in res:
+        for i in range(y.shape[0]):
+            got[first + i] = y[i]
+    assert sorted(got) == list(range(B5))
+    for b in range(B5):
+        want = O.mix_s16(_tracks5(b), RAMPS5)
+        assert np.array_equal(got[b], want), b

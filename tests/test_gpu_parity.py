@@ -318,3 +318,58 @@ def test_resample_only_batches(xm, gpu, B, N):
     idx = range(B) if N < 100000 else (0, 7, 8, 15)
     for b in idx:
         assert bits_equal(y[b], CO.resample_f32(x[b, 0], 147, 160)), b
+
+
+SPAN_RAMPS = [dict(gain0_q15=q, gain1_q15=q2, ramp_start=s, ramp_len=ln, mode=md)
+              for q, q2, s, ln, md in [(32768, 32768, 0, 0, 0), (0, 32768, 100, 20000, 0), (65535, 100, 0, 9600, 0),
+                                       (16384, 16384, 0, 0, 0), (0, 0, 5000, 900, 1), (0, 32768, 5000, 900, 0),
+                                       (40000, 3, 7000, 13, 0), (7, 60000, 4800, 0, 0)] * 2]
+
+
+@pytest.mark.parametrize("rate_out", [48000, 44100])
+def test_partial_finish_s16_spanning(xm, gpu, rate_out):
+    """Config 5 kernels: the 16 tracks of every mix split over two handles (as
+    over two devices); int32 partials (vs the numpy oracle), summed by
+    finish_s16 in part order, equal the one-handle 16-track mix bit for bit.
+    rate_out 44100 runs the partial through the resampling (generic) kernel."""
+    import torch
+    B, N, ntr = 3, 9600, 16
+    x = np.stack([np.stack([O.gen_s16(SEED, 5000 + 16 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    x[:, :4, 100:300] = 32767       # the full mix saturates there
+    full = xm.Mixer(48000, rate_out, 2, "s16")
+    full.set_tracks(SPAN_RAMPS)
+    ref = full.process(x)
+    F = full.out_frames(N)
+    xd = torch.from_numpy(x).cuda()
+    parts = torch.zeros((2, B, F * 2), dtype=torch.int32, device="cuda")
+    for h in range(2):
+        m = xm.Mixer(48000, rate_out, 2, "s16", mem="device")
+        m.set_tracks(SPAN_RAMPS[8 * h: 8 * h + 8])
+        xh = xd[:, 8 * h: 8 * h + 8].contiguous()
+        m.process_partial_strided(xh.data_ptr(), N * 2, 8 * N * 2, parts[h].data_ptr(), F * 2, B, N)
+        torch.cuda.synchronize()
+        if rate_out == 48000:
+            for b in range(B):
+                want = O.mix_s16_partial(list(x[b, 8 * h: 8 * h + 8]), SPAN_RAMPS[8 * h: 8 * h + 8]).reshape(-1)
+                assert bits_equal(parts[h, b].cpu().numpy(), want), (h, b)
+    y = torch.empty((B, F, 2), dtype=torch.int16, device="cuda")
+    m.finish_s16(parts.data_ptr(), 2, B * F * 2, F * 2, y.data_ptr(), F * 2, B, F)
+    assert bits_equal(y.cpu().numpy(), ref)
+    if rate_out == 48000:
+        assert bits_equal(ref, CO.batch_mix_s16(x, SPAN_RAMPS, threads=4)[0])
+    # the exchange's own form: one pre-summed partial, saturate only
+    summed = (parts[0] + parts[1]).contiguous()
+    y1 = torch.empty_like(y)
+    m.finish_s16(summed.data_ptr(), 1, 0, F * 2, y1.data_ptr(), F * 2, B, F)
+    assert bits_equal(y1.cpu().numpy(), ref)
+
+
+def test_partial_errors(xm, gpu):
+    m = xm.Mixer(48000, 48000, 2, "f32", mem="device")
+    with pytest.raises(xm.XmError) as e:
+        m.process_partial_strided(1, 2, 2, 1, 2, 1, 1)
+    assert e.value.code == xm.XM_ENOSYS
+    h = xm.Mixer(48000, 48000, 2, "s16")     # host memory: not supported
+    with pytest.raises(xm.XmError) as e:
+        h.finish_s16(1, 1, 0, 2, 1, 2, 1, 1)
+    assert e.value.code == xm.XM_ENOSYS

@@ -8,6 +8,8 @@ c2  48k->44.1k resample, 4096 stereo 10 s fp32 clips (1-track mixes, unity gain)
 c3  8-track s16 Q15 gain-ramp + crossfade mix, 1024 mixes x 10 s stereo 48 kHz
 c4  per-GPU shard of config 4: 1024 clips = 128 mixes x 8 tracks, resample ->
     5-band RBJ EQ (biquad cascade) -> gain -> mix (8192 clips over 8 GPUs)
+c5  config 5 on this GPU: 512 mixes x 8 of their 64 s16 tracks -> int32 partial
+    -> reduce-scatter over RCCL when launched with torchrun -> saturate
 Unit: input samples (frames x channels x tracks) per second; roofline
 fraction = algorithmic bytes (inputs once + output once) / kernel time / 8 TB/s.
 Inputs are synthetic PCM generated in HBM (xm_synth_pcm), outside the timing.
@@ -110,6 +112,32 @@ def c4(a):
            B * ntr * N * 2, B * ntr * N * 8 + B * F * 8, w, k, m)
 
 
+def c5(a):
+    """Config 5 per GPU: 8 of the 64 s16 tracks of every mix live here; int32
+    partial -> RCCL reduce-scatter (torchrun, N > 1) -> saturate."""
+    from xmaudio import dist as xd
+    rk = xd.from_env()
+    dev = rk.local
+    torch.cuda.set_device(dev)
+    xd.init(rk, "nccl", torch.device("cuda", dev))
+    B, ntr, N = a.mixes5, 8, 480000
+    m = xm.Mixer(48000, 48000, 2, "s16", mem="device", device=dev)
+    m.set_tracks(Q15_RAMPS)
+    s = torch.cuda.current_stream()
+    m.set_stream(s.cuda_stream)
+    x = torch.empty((B, ntr, N, 2), dtype=torch.int16, device="cuda")
+    xm.synth(x.data_ptr(), "s16", SEED, rk.rank * B * ntr, B * ntr, 2, N, dev, s.cuda_stream)
+    y = torch.empty((B // rk.world, N, 2), dtype=torch.int16, device="cuda")
+    w, k = timed(lambda: xd.mix_spanning_s16(rk, m, x, out=y), a.steps, a.warmup, s)
+    w = xd.max_over_ranks(rk, w, device="cuda")
+    if rk.rank == 0:
+        report("c5", f"64-track s16 mixdown, {B} mixes x 10 s stereo 48 kHz, 8 tracks per GPU, "
+                     f"{rk.world} GPU(s) (partial + reduce-scatter + saturate)",
+               rk.world * B * ntr * N * 2, B * ntr * N * 4 + (B // rk.world) * N * 4, w, k, m,
+               note="per-GPU HBM bytes: this GPU's tracks once + its finished mixes once")
+    xd.finish(rk)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("which", nargs="*", default=["c2", "c3", "c4"])
@@ -118,6 +146,7 @@ def main():
     ap.add_argument("--clips", type=int, default=4096)
     ap.add_argument("--mixes3", type=int, default=1024)
     ap.add_argument("--mixes4", type=int, default=128)
+    ap.add_argument("--mixes5", type=int, default=512)
     a = ap.parse_args()
     for w in a.which:
         globals()[w](a)

@@ -18,7 +18,8 @@ constexpr int GEN_CHUNK = GEN_THREADS * GEN_OPT;    // output frames per block
 // chunk needs into LDS (zero outside [0, N) — equivalent to scipy's skip, see
 // DESIGN.md "zero padding"), then each thread forms its outputs tap by tap in
 // ascending order (oldest input first) exactly as upfirdn does.
-template <int C, bool S16>
+// PART (s16, config 5): write the int32 track sum instead of the saturated mix
+template <int C, bool S16, bool PART = false>
 __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob j)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -92,7 +93,11 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
     for (int o = 0; o < GEN_OPT; ++o) {
         const int64_t m = m0 + threadIdx.x + o * GEN_THREADS;
         if (m >= m1) continue;
-        if (S16) {
+        if (S16 && PART) {
+            int32_t *y = (int32_t *)xm_out_ptr(j, b, 4);
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[m * C + c] = acci[o][c];
+        } else if (S16) {
             int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
 #pragma unroll
             for (int c = 0; c < C; ++c) y[m * C + c] = xm_sat16(acci[o][c]);
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
 // them once.
 constexpr int MIX_THREADS = 256;
 
-template <int C>
+template <int C, bool PART = false>
 __global__ __launch_bounds__(MIX_THREADS) void k_mix_s16(XmhMixJob j)
 {
     constexpr int SPT = 8;                 // samples per thread (16 B)
@@ -151,6 +156,20 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_s16(XmhMixJob j)
                 for (int c = 0; c < C; ++c) acc[f * C + c] += xm_q15_term(v[f * C + c], gq);
             }
         }
+    }
+    if constexpr (PART) {   // config 5 partial: the int32 sum, saturated later by k_finish_s16
+        int32_t *yp = (int32_t *)xm_out_ptr(j, b, 4) + s0;
+        if (full && ((((uintptr_t)yp) & 15) == 0)) {
+            int4 q0, q1;
+            __builtin_memcpy(&q0, acc, 16);
+            __builtin_memcpy(&q1, acc + 4, 16);
+            ((int4 *)yp)[0] = q0;
+            ((int4 *)yp)[1] = q1;
+        } else {
+            for (int i = 0; i < SPT; ++i)
+                if (s0 + i < total) yp[i] = acc[i];
+        }
+        return;
     }
     int16_t o[SPT];
 #pragma unroll
@@ -208,6 +227,46 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_f32(XmhMixJob j)
     }
 }
 
+// Config 5 finish: out = sat16(sum of n_parts int32 partials, in part order).
+// 8 samples (32 B of each partial, 16 B out) per thread, coalesced.
+__global__ __launch_bounds__(MIX_THREADS) void k_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride,
+                                                          int64_t part_mix_stride, int16_t *out,
+                                                          int64_t out_mix_stride, int64_t samples)
+{
+    constexpr int SPT = 8;
+    const int64_t b = blockIdx.y;
+    const int64_t s0 = ((int64_t)blockIdx.x * MIX_THREADS + threadIdx.x) * SPT;
+    if (s0 >= samples) return;
+    const int32_t *p = parts + b * part_mix_stride + s0;
+    int16_t *y = out + b * out_mix_stride + s0;
+    const bool vec = s0 + SPT <= samples && ((((uintptr_t)p) | ((uintptr_t)y)) & 15) == 0 &&
+                     ((part_stride * 4) & 15) == 0;
+    int32_t acc[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) acc[i] = 0;
+    for (int q = 0; q < n_parts; ++q, p += part_stride) {
+        if (vec) {
+            const int4 a0 = ((const int4 *)p)[0], a1 = ((const int4 *)p)[1];
+            acc[0] += a0.x; acc[1] += a0.y; acc[2] += a0.z; acc[3] += a0.w;
+            acc[4] += a1.x; acc[5] += a1.y; acc[6] += a1.z; acc[7] += a1.w;
+        } else {
+            for (int i = 0; i < SPT; ++i)
+                if (s0 + i < samples) acc[i] += p[i];
+        }
+    }
+    int16_t o[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) o[i] = xm_sat16(acc[i]);
+    if (vec) {
+        int4 qv;
+        __builtin_memcpy(&qv, o, 16);
+        *(int4 *)y = qv;
+    } else {
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < samples) y[i] = o[i];
+    }
+}
+
 template <typename K>
 int launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const XmhMixJob &j)
 {
@@ -229,14 +288,17 @@ extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
     const int C = j->channels;
     const bool s16 = j->fmt == 1;
     if (j->frames_out == 0 || j->n_mix == 0) return 0;
+    if (j->partial && !s16) return -22;   // XM_EINVAL: partials are the s16 (Q15) mix
     if (j->rs.L == j->rs.M) {
         const int spt = s16 ? 8 : 4;
         const int64_t samples = j->frames_out * C;
         dim3 grid((unsigned)((samples + (int64_t)MIX_THREADS * spt - 1) / ((int64_t)MIX_THREADS * spt)),
                   (unsigned)j->n_mix);
         int rc;
-        if (s16) rc = C == 1 ? launch(k_mix_s16<1>, grid, MIX_THREADS, 0, s, *j)
-                             : launch(k_mix_s16<2>, grid, MIX_THREADS, 0, s, *j);
+        if (s16 && j->partial) rc = C == 1 ? launch(k_mix_s16<1, true>, grid, MIX_THREADS, 0, s, *j)
+                                           : launch(k_mix_s16<2, true>, grid, MIX_THREADS, 0, s, *j);
+        else if (s16) rc = C == 1 ? launch(k_mix_s16<1>, grid, MIX_THREADS, 0, s, *j)
+                                  : launch(k_mix_s16<2>, grid, MIX_THREADS, 0, s, *j);
         else     rc = C == 1 ? launch(k_mix_f32<1>, grid, MIX_THREADS, 0, s, *j)
                              : launch(k_mix_f32<2>, grid, MIX_THREADS, 0, s, *j);
         if (n_launches) *n_launches += 1;
@@ -248,10 +310,27 @@ extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
     if (lds > 160 * 1024) return -1003;  // XM_ENOSYS: ratio too extreme for the LDS-staged path
     dim3 grid((unsigned)((j->frames_out + GEN_CHUNK - 1) / GEN_CHUNK), (unsigned)j->n_mix);
     int rc;
-    if (s16) rc = C == 1 ? launch(k_resample_mix_generic<1, true>, grid, GEN_THREADS, lds, s, *j)
-                         : launch(k_resample_mix_generic<2, true>, grid, GEN_THREADS, lds, s, *j);
+    if (s16 && j->partial) rc = C == 1 ? launch(k_resample_mix_generic<1, true, true>, grid, GEN_THREADS, lds, s, *j)
+                                       : launch(k_resample_mix_generic<2, true, true>, grid, GEN_THREADS, lds, s, *j);
+    else if (s16) rc = C == 1 ? launch(k_resample_mix_generic<1, true>, grid, GEN_THREADS, lds, s, *j)
+                              : launch(k_resample_mix_generic<2, true>, grid, GEN_THREADS, lds, s, *j);
     else     rc = C == 1 ? launch(k_resample_mix_generic<1, false>, grid, GEN_THREADS, lds, s, *j)
                          : launch(k_resample_mix_generic<2, false>, grid, GEN_THREADS, lds, s, *j);
     if (n_launches) *n_launches += 1;
     return rc;
+}
+
+extern "C" int xmh_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
+                                     int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream)
+{
+    if (batch <= 0 || samples <= 0) return 0;
+    const unsigned gx = (unsigned)((samples + (int64_t)MIX_THREADS * 8 - 1) / ((int64_t)MIX_THREADS * 8));
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {   // grid.y limit
+        const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+        hipLaunchKernelGGL(k_finish_s16, dim3(gx, (unsigned)nb), dim3(MIX_THREADS), 0, (hipStream_t)stream,
+                           parts + b0 * part_mix_stride, n_parts, part_stride, part_mix_stride,
+                           out + b0 * out_mix_stride, out_mix_stride, samples);
+        if (hipGetLastError() != hipSuccess) return -1001;
+    }
+    return 0;
 }

@@ -58,7 +58,7 @@ typedef struct XmhMixJob {
     const XmhGain *gains;     /* device, n_tracks entries */
     const XmhGain *gains_host; /* host copy (kernel-argument path), n_tracks entries */
     int32_t unity;            /* 1: every gain is constant 1.0 (pure resample fast path) */
-    int32_t reserved;
+    int32_t partial;          /* s16 only: 1 = write the int32 track sum, no saturation (config 5) */
     XmhResample rs;
     /* optional per-track effects chain (config 4): device sos table */
     const float *sos;         /* n_sos x 6, or NULL */
@@ -108,6 +108,9 @@ const char *xmh_arch_name(void);
 /* resample (if rs.L != rs.M) + gain + ordered track sum; returns launches made */
 int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches);
 int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
+/* config 5 finish: out[b][i] = sat16(sum over p of parts[p*part_stride + b*part_mix_stride + i]) */
+int xmh_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
+                          int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream);
 /* 0 if the phase-major table H (L x T) equals, bit for bit, the coefficients
  * baked into the 147/160 fast kernel (tools/gen_coefs.c); -1003 otherwise */
 int xmh_fast_table_check(const float *H, int L, int M, int T);

@@ -470,6 +470,53 @@ int xm_audio_mixer_process_batch(XmAudioMixer *m, const void *const *in, void *c
     return finish(m, rc);
 }
 
+int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in, ptrdiff_t in_track_stride,
+                                       ptrdiff_t in_mix_stride, int32_t *partial, ptrdiff_t partial_mix_stride,
+                                       size_t batch, size_t frames_in)
+{
+    if (!m || (batch && (!in || !partial))) return XM_EINVAL;
+    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx) return XM_ENOSYS;
+    if (batch == 0) return XM_OK;
+    if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    memset(&m->timing, 0, sizeof m->timing);
+    if ((rc = upload_gains(m))) return rc;
+    if (xm_audio_mixer_out_frames(m, frames_in) == 0) return XM_OK;
+    XmhMixJob j;
+    job_init(m, &j, batch, frames_in);
+    j.in = in;
+    j.in_track_stride = in_track_stride;
+    j.in_mix_stride = in_mix_stride;
+    j.out = partial;
+    j.out_mix_stride = partial_mix_stride;
+    j.partial = 1;
+    rc = run_job(m, &j);
+    return finish(m, rc);
+}
+
+int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, int n_parts, ptrdiff_t part_stride,
+                              ptrdiff_t partial_mix_stride, int16_t *out, ptrdiff_t out_mix_stride, size_t batch,
+                              size_t out_frames)
+{
+    if (!m || n_parts < 1 || n_parts > XM_MAX_TRACKS) return XM_EINVAL;
+    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE) return XM_ENOSYS;
+    if (batch == 0 || out_frames == 0) return XM_OK;
+    if (!partials || !out || batch > (size_t)INT32_MAX) return XM_EINVAL;
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    memset(&m->timing, 0, sizeof m->timing);
+    rc = xmh_event_record(m->ev[2], m->stream);
+    if (!rc)
+        rc = xmh_launch_finish_s16(partials, n_parts, part_stride, partial_mix_stride, out, out_mix_stride,
+                                   (int64_t)batch, (int64_t)out_frames * m->cfg.channels, m->stream);
+    if (!rc) {
+        m->timing.n_launches = 1;
+        rc = xmh_event_record(m->ev[3], m->stream);
+    }
+    return finish(m, rc);
+}
+
 int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in_track_stride,
                                    ptrdiff_t in_mix_stride, void *out, ptrdiff_t out_mix_stride, size_t batch,
                                    size_t frames_in)

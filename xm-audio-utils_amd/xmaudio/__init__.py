@@ -52,6 +52,7 @@ EXPORTED = [
     "xm_audio_mixer_set_crossfade", "xm_audio_mixer_set_track_effects", "xm_audio_mixer_out_frames",
     "xm_audio_mixer_set_stream", "xm_audio_mixer_process_batch", "xm_audio_mixer_process_strided",
     "xm_audio_mixer_get_timing", "xm_audio_mixer_freep",
+    "xm_audio_mixer_process_partial_s16", "xm_audio_mixer_finish_s16",
     "xm_effects_create_ex", "xm_effects_create", "xm_effects_add_biquad", "xm_effects_add_eq_band",
     "xm_effects_add_fir", "xm_effects_count", "xm_effects_get_biquad", "xm_effects_set_stream",
     "xm_effects_process_batch", "xm_effects_freep",
@@ -103,6 +104,8 @@ _sigs = {
     "xm_audio_mixer_process_batch": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), _sz, _sz]),
     "xm_audio_mixer_process_strided": (_i, [_vp, _vp, C.c_ssize_t, C.c_ssize_t, _vp, C.c_ssize_t, _sz, _sz]),
     "xm_audio_mixer_get_timing": (_i, [_vp, C.POINTER(XmMixerTiming)]),
+    "xm_audio_mixer_process_partial_s16": (_i, [_vp, _vp, C.c_ssize_t, C.c_ssize_t, _vp, C.c_ssize_t, _sz, _sz]),
+    "xm_audio_mixer_finish_s16": (_i, [_vp, _vp, _i, C.c_ssize_t, C.c_ssize_t, _vp, C.c_ssize_t, _sz, _sz]),
     "xm_audio_mixer_freep": (None, [C.POINTER(_vp)]),
     "xm_effects_create_ex": (_vp, [C.POINTER(XmEffectsConfig), C.POINTER(_i)]),
     "xm_effects_add_biquad": (_i, [_vp, C.POINTER(C.c_float)]),
@@ -253,6 +256,20 @@ class Mixer:
                         out_mix_stride: int, batch: int, frames_in: int):
         _check(_lib.xm_audio_mixer_process_strided(self._h, in_ptr, in_track_stride, in_mix_stride, out_ptr,
                                                    out_mix_stride, batch, frames_in), "process_strided")
+
+
+    def process_partial_strided(self, in_ptr: int, in_track_stride: int, in_mix_stride: int, partial_ptr: int,
+                                partial_mix_stride: int, batch: int, frames_in: int):
+        """Config 5: int32 Q15 partial sum of this handle's tracks (device memory)."""
+        _check(_lib.xm_audio_mixer_process_partial_s16(self._h, in_ptr, in_track_stride, in_mix_stride,
+                                                       partial_ptr, partial_mix_stride, batch, frames_in),
+               "process_partial_s16")
+
+    def finish_s16(self, partials_ptr: int, n_parts: int, part_stride: int, partial_mix_stride: int,
+                   out_ptr: int, out_mix_stride: int, batch: int, out_frames: int):
+        """Config 5: saturate the (summed) partials to s16 (device memory)."""
+        _check(_lib.xm_audio_mixer_finish_s16(self._h, partials_ptr, n_parts, part_stride, partial_mix_stride,
+                                              out_ptr, out_mix_stride, batch, out_frames), "finish_s16")
 
 
 class Effects:

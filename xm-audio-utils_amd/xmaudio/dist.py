@@ -3,8 +3,10 @@
 Mixes are independent, so N GPUs are N processes, each owning a contiguous
 block of mixes (weak scaling: a fixed block per rank) with no collective in
 the data path.  torch.distributed (RCCL = backend "nccl" on ROCm, or "gloo"
-on CPU for tests) is used only for the start/stop barriers and the
-max-over-ranks wall time.
+on CPU for tests) is used for the start/stop barriers and the max-over-ranks
+wall time, and for the one real exchange of the path: config 5
+(BASELINE.json:11), where the tracks of every mix are spread over the ranks
+and the int32 partial sums meet in a reduce-scatter (reduce_partials).
 """
 from __future__ import annotations
 
@@ -45,6 +47,54 @@ def mix_block(r: Rank, mixes_per_rank: int) -> tuple[int, int]:
 def first_clip(r: Rank, mixes_per_rank: int, tracks: int) -> int:
     """Global clip id of track 0 of this rank's first mix (clip = mix*tracks + track)."""
     return mix_block(r, mixes_per_rank)[0] * tracks
+
+
+def owned_mixes(r: Rank, batch: int) -> tuple[int, int]:
+    """Config 5: (first, count) of the mixes rank r finishes after the exchange."""
+    if batch % r.world:
+        raise ValueError(f"batch {batch} does not divide over {r.world} ranks")
+    n = batch // r.world
+    return r.rank * n, n
+
+
+def reduce_partials(r: Rank, part):
+    """Config 5 exchange.  `part` is this rank's [batch, S] int32 Q15 partial
+    (xm_audio_mixer_process_partial_s16 over the tracks it holds); returns the
+    [batch/world, S] block of the mixes owned_mixes() gives this rank, summed
+    over every rank.  int32 sums of <= 64 Q15 terms cannot overflow, so any
+    order is exact and RCCL's reduce-scatter (its own schedule over xGMI) is
+    bit-exact.  gloo (the CPU tests) gets the same block from an all-reduce."""
+    if r.world <= 1:
+        return part
+    import torch
+    import torch.distributed as dist
+    first, n = owned_mixes(r, part.shape[0])
+    part = part.contiguous()
+    if dist.get_backend() == "gloo":
+        full = part.clone()
+        dist.all_reduce(full, op=dist.ReduceOp.SUM)
+        return full[first:first + n].contiguous()
+    out = torch.empty((n,) + tuple(part.shape[1:]), dtype=part.dtype, device=part.device)
+    dist.reduce_scatter_tensor(out, part, op=dist.ReduceOp.SUM)
+    return out
+
+
+def mix_spanning_s16(r: Rank, mixer, x, out=None):
+    """Config 5 on this rank.  x: [batch, tracks_here, frames, C] int16 in HBM,
+    this rank's tracks of every mix (mixer.set_tracks holds their ramps).
+    Returns [batch/world, out_frames, C] int16: the finished mixes
+    owned_mixes() gives this rank (partial -> reduce_partials -> finish)."""
+    import torch
+    B, T, F, C = x.shape
+    Fo = mixer.out_frames(F)
+    part = torch.empty((B, Fo * C), dtype=torch.int32, device=x.device)
+    mixer.process_partial_strided(x.data_ptr(), F * C, T * F * C, part.data_ptr(), Fo * C, B, F)
+    blk = reduce_partials(r, part)
+    n = blk.shape[0]
+    if out is None:
+        out = torch.empty((n, Fo, C), dtype=torch.int16, device=x.device)
+    mixer.finish_s16(blk.data_ptr(), 1, 0, Fo * C, out.data_ptr(), Fo * C, n, Fo)
+    return out
 
 
 def barrier(r: Rank) -> None:
