@@ -121,6 +121,31 @@ XM_API int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, i
                               int16_t *out, ptrdiff_t out_mix_stride,
                               size_t batch, size_t out_frames);
 
+/* ---- streaming (build-owned) ----------------------
+ * `batch` mixes whose tracks arrive in blocks.  stream_begin() starts them at
+ * input frame 0; every stream_push() appends the next frames_in frames of
+ * every track (layout as process_strided, strides in elements) and writes the
+ * output frames that no later input can change, *frames_out of them, to
+ * out + b*out_mix_stride (out_cap: the room per mix, in frames);
+ * stream_flush() ends the signal (N = all frames pushed) and writes the
+ * rest.  The concatenated outputs equal one process_* call over the whole
+ * signal, bit for bit, for any split into blocks (ragged, 1-frame, empty):
+ * each output is computed by the same taps, in the same order, with the gain
+ * ramp at the same absolute output frame.  The handle keeps the input frames
+ * the next output still needs (about T + M/L frames per track) on the device.
+ * stream_out_frames(frames_in, flush) is the exact count the next push of
+ * frames_in frames (flush = 0) or the flush (flush = 1, frames_in = 0) writes.
+ * Not with per-track effects (XM_ENOSYS: stream those with
+ * xm_effects_process_stream); set_tracks with another track count ends the
+ * stream (XM_EINVAL until stream_begin). */
+XM_API int xm_audio_mixer_stream_begin(XmAudioMixer *m, size_t batch);
+XM_API size_t xm_audio_mixer_stream_out_frames(const XmAudioMixer *m, size_t frames_in, int flush);
+XM_API int xm_audio_mixer_stream_push(XmAudioMixer *m, const void *in, ptrdiff_t in_track_stride,
+                               ptrdiff_t in_mix_stride, size_t frames_in, void *out,
+                               ptrdiff_t out_mix_stride, size_t out_cap, size_t *frames_out);
+XM_API int xm_audio_mixer_stream_flush(XmAudioMixer *m, void *out, ptrdiff_t out_mix_stride,
+                                size_t out_cap, size_t *frames_out);
+
 XM_API int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t);
 
 /* Destroy and NULL the handle (no-op on NULL). */

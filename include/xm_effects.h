@@ -64,6 +64,21 @@ XM_API int xm_effects_set_stream(XmEffects *e, void *hip_stream);
 XM_API int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const *out,
                              size_t batch, size_t frames);
 
+/* ---- streaming (build-owned) ----------------------
+ * n_clips long signals fed in blocks.  xm_effects_stream_reset() (re)starts
+ * n_clips streams at zero state for the chain as it is now; every
+ * xm_effects_process_stream() call filters the next `frames` frames of each
+ * stream (in[i] / out[i] as process_batch, in == out allowed), carrying on
+ * the device the biquad state (z0, z1 per section and channel) and the last
+ * K-1 input frames of every FIR stage.  Any split of a signal into blocks
+ * (ragged, 1-frame or empty blocks) gives, bit for bit, the output of one
+ * process_batch() over the whole signal.  Adding an effect ends the streams:
+ * process_stream then fails with XM_EINVAL until the next reset, as it does
+ * for an n_clips other than the reset's. */
+XM_API int xm_effects_stream_reset(XmEffects *e, size_t n_clips);
+XM_API int xm_effects_process_stream(XmEffects *e, const float *const *in, float *const *out,
+                              size_t n_clips, size_t frames);
+
 XM_API void xm_effects_freep(XmEffects **e);
 
 #ifdef __cplusplus

@@ -1,0 +1,175 @@
+"""GPU parity of the streaming entry points:
+xm_audio_mixer_stream_{begin,push,flush} and xm_effects_{stream_reset,
+process_stream}.  A signal split into ragged blocks (1-frame, empty, shorter
+than the filter history, longer than a kernel chunk) must give, bit for bit,
+the oracle's output for the whole signal — and so the whole-signal GPU call."""
+import numpy as np
+import pytest
+
+from conftest import bits_equal, golden, ulp_diff
+
+import c_oracle as CO
+import np_oracle as O
+
+pytestmark = pytest.mark.gpu
+SEED = O.SEED
+
+RAMPS8 = [
+    dict(gain0=0.9), dict(gain0=0.0, gain1=0.8, ramp_start=100, ramp_len=3000),
+    dict(gain0=0.7, gain1=0.2, ramp_start=2000, ramp_len=441), dict(gain0=0.5),
+    dict(mode=1, ramp_start=3000, ramp_len=800), dict(gain0=0.0, gain1=1.0, ramp_start=3000, ramp_len=800),
+    dict(gain0=1.25, gain1=0.75, ramp_start=0, ramp_len=4410), dict(gain0=0.3, gain1=0.6, ramp_start=4000),
+]
+
+
+def _blocks(N, pattern):
+    """Block sizes summing to N: the pattern, then 4099-frame blocks, then the rest."""
+    out, left = [], N
+    for b in pattern:
+        b = min(b, left)
+        out.append(b)
+        left -= b
+    while left > 0:
+        out.append(min(4099, left))
+        left -= out[-1]
+    return out
+
+
+PATTERNS = {
+    "ragged": [0, 1, 5, 137, 0, 1000, 17, 2, 33],
+    "single_frames": [1] * 40 + [0, 3],
+    "one_block": [10 ** 9],
+}
+
+
+def _stream_mix(m, x, sizes):
+    B = x.shape[0]
+    m.stream_begin(B)
+    outs, p = [], 0
+    for n in sizes:
+        outs.append(m.stream_push(x[:, :, p:p + n]))
+        p += n
+    assert p == x.shape[2]
+    outs.append(m.stream_flush())
+    return np.concatenate(outs, axis=1)
+
+
+@pytest.mark.parametrize("pattern", sorted(PATTERNS))
+def test_stream_resample_mix_f32_48_to_44(xm, gpu, pattern):
+    B, ntr, N = 2, 8, 9600 + 77
+    x = np.stack([np.stack([O.gen_f32(SEED, 3000 + 8 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(RAMPS8)
+    y = _stream_mix(m, x, _blocks(N, PATTERNS[pattern]))
+    ref, _ = CO.batch_resample_mix_f32(x, RAMPS8, 147, 160, threads=4)
+    assert y.shape == ref.shape
+    assert bits_equal(y, ref), f"max ulp {ulp_diff(y, ref)}"
+    assert bits_equal(y, m.process(x))
+
+
+def test_stream_resample_s16_44_to_48_mono(xm, gpu):
+    N = 8820 + 3
+    x = np.stack([O.gen_s16(SEED, 3100 + t, 1, N) for t in range(3)])[None]
+    ramps = RAMPS8[1:4]
+    m = xm.Mixer(44100, 48000, 1, "s16")
+    m.set_tracks(ramps)
+    y = _stream_mix(m, x, _blocks(N, PATTERNS["ragged"]))
+    ref = CO.resample_mix_s16(list(x[0]), ramps, 160, 147)
+    assert bits_equal(y[0], ref.reshape(y[0].shape))
+
+
+def test_stream_mix_s16_same_rate(xm, gpu):
+    """Config 3 mixer (no resampling) streamed: gains at the absolute frame."""
+    N = 6000 + 5
+    x = np.stack([np.stack([O.gen_s16(SEED, 3200 + 8 * b + t, 2, N) for t in range(8)]) for b in range(2)])
+    m = xm.Mixer(48000, 48000, 2, "s16")
+    m.set_tracks(RAMPS8)
+    y = _stream_mix(m, x, _blocks(N, [0, 1, 7, 301, 2, 999]))
+    for b in range(2):
+        assert bits_equal(y[b], CO.mix_s16(list(x[b]), RAMPS8).reshape(y[b].shape))
+
+
+def test_stream_device_memory_strided(xm, gpu):
+    import torch
+    B, ntr, N = 2, 8, 9600
+    x = np.stack([np.stack([O.gen_f32(SEED, 3300 + 8 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    ref = xm.Mixer(48000, 44100, 2, "f32")
+    ref.set_tracks(RAMPS8)
+    want = ref.process(x)
+    dev = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    dev.set_tracks(RAMPS8)
+    F = dev.out_frames(N)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.zeros((B, F, 2), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    dev.stream_begin(B)
+    got = 0
+    for p0, n in zip(np.cumsum([0] + _blocks(N, [3, 500, 1])[:-1]), _blocks(N, [3, 500, 1])):
+        got += dev.stream_push_strided(xd[:, :, int(p0):].data_ptr(), N * 2, ntr * N * 2, n,
+                                       yd[:, got:].data_ptr(), F * 2, F - got)
+    got += dev.stream_flush_strided(yd[:, got:].data_ptr(), F * 2, F - got)
+    assert got == F
+    assert bits_equal(yd.cpu().numpy(), want)
+
+
+def test_stream_mixer_errors(xm, gpu):
+    import ctypes
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m._st_batch = 1
+    with pytest.raises(xm.XmError):   # push before begin
+        m.stream_push(np.zeros((1, 1, 10, 2), np.float32))
+    m.stream_begin(1)
+    x = np.zeros((1, 1, 4000, 2), np.float32)
+    y = np.zeros((1, 10, 2), np.float32)
+    n = ctypes.c_size_t(0)
+    rc = xm._lib.xm_audio_mixer_stream_push(m._h, x.ctypes.data, 8000, 8000, 4000, y.ctypes.data, 20, 10,
+                                           ctypes.byref(n))
+    assert rc == xm.XM_EINVAL and n.value == 0   # out_cap too small: nothing consumed
+    assert m.stream_push(x).shape[1] == -(-4000 * 147 // 160) - 11   # ceil(L*R/M) - rm
+    m.set_tracks([dict(gain0=1.0), dict(gain0=1.0)])
+    with pytest.raises(xm.XmError):   # track count changed mid-stream
+        m.stream_push(np.zeros((1, 2, 10, 2), np.float32))
+
+
+@pytest.mark.parametrize("channels", [1, 2])
+@pytest.mark.parametrize("pattern", ["ragged", "single_frames", "chunk_edges"])
+def test_effects_stream_chain(xm, gpu, channels, pattern):
+    """biquad x3 -> FIR 63 -> biquad x2, streamed, against the whole-signal oracle."""
+    z = golden("effects.npz")
+    B, N = 5, 6000 + 11
+    x = np.stack([O.gen_f32(SEED, 3400 + b, channels, N) for b in range(B)])
+    e = xm.Effects(48000, channels)
+    for s in z["sos"][:3]:
+        e.add_biquad(s)
+    e.add_fir(z["h63"])
+    for s in z["sos"][3:]:
+        e.add_biquad(s)
+    pat = {"ragged": PATTERNS["ragged"], "single_frames": PATTERNS["single_frames"],
+           "chunk_edges": [31, 32, 33, 62, 64, 65, 1, 127]}[pattern]
+    e.stream_reset(B)
+    outs, p = [], 0
+    for i, n in enumerate(_blocks(N, pat)):
+        outs.append(e.process_stream(x[:, p:p + n], inplace=(i % 3 == 2)))
+        p += n
+    y = np.concatenate(outs, axis=1)
+    for b in range(B):
+        r = CO.biquad_f32(CO.fir_f32(CO.biquad_f32(x[b], z["sos"][:3]), z["h63"]), z["sos"][3:])
+        assert bits_equal(y[b], r), (b, ulp_diff(y[b], r))
+    # the stream ends when the chain changes; a reset restarts from zero state
+    e.add_fir(np.array([1.0], np.float32))
+    with pytest.raises(xm.XmError):
+        e.process_stream(x[:, :10])
+    e.stream_reset(B)
+    y2 = e.process_stream(x)
+    assert bits_equal(y2, e.process(x))
+
+
+def test_effects_stream_errors(xm, gpu):
+    e = xm.Effects(48000, 2)
+    e.add_biquad(golden("effects.npz")["sos"][0])
+    x = np.zeros((2, 100, 2), np.float32)
+    with pytest.raises(xm.XmError):   # no reset
+        e.process_stream(x)
+    e.stream_reset(3)
+    with pytest.raises(xm.XmError):   # clip count differs from the reset
+        e.process_stream(x)

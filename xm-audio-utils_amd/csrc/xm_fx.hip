@@ -36,7 +36,7 @@ template <>
 struct BqVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
 typedef float bq_f4 __attribute__((ext_vector_type(4)));
 
-template <int C, int CH>
+template <int C, int CH, bool ST>
 __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
 {
     typedef typename BqVec<C>::T V;
@@ -62,6 +62,11 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
     const float *q = j.sos + 6 * s;                 // this lane's section, state zero at clip start
     const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
     V z0 = V(0.0f), z1 = V(0.0f);
+    float *st = (ST && valid) ? j.state + ((size_t)clip * ns + s) * 2 * C : nullptr;
+    if (ST && st) {                                // streaming: continue from the previous block
+        if constexpr (C == 2) { z0 = V{st[0], st[1]}; z1 = V{st[2], st[3]}; }
+        else { z0 = st[0]; z1 = st[1]; }
+    }
 
     bq_f4 pa[G], pb[G];                            // section 0: chunks i and i + 1 in flight
     auto load = [&](bq_f4 (&d)[G], int64_t c) {
@@ -89,6 +94,9 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
 #pragma unroll
         for (int g = 0; g < G; ++g) v4[g] = src[g * 64];
         if (c >= 0 && c < nchunk) {
+            // the last chunk's frames past N are zero padding: with a state
+            // to carry they must not advance the recurrence
+            const bool tail = ST && st && (c + 1) * CH > N;
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 bq_f4 r;
@@ -98,8 +106,12 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
                     if constexpr (C == 2) v = V{v4[g][2 * e], v4[g][2 * e + 1]};
                     else v = v4[g][e];
                     const V o = b0 * v + z0;              // sosfilt (_sosfilt.pyx) order
-                    z0 = (b1 * v - a1 * o) + z1;
-                    z1 = b2 * v - a2 * o;
+                    if (tail && c * CH + g * FPL + e >= N) {
+                        // padding frame: output unused, state kept
+                    } else {
+                        z0 = (b1 * v - a1 * o) + z1;
+                        z1 = b2 * v - a2 * o;
+                    }
                     if constexpr (C == 2) { r[2 * e] = o.x; r[2 * e + 1] = o.y; }
                     else r[e] = o;
                 }
@@ -130,6 +142,10 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
         step(i, pa);
         if (i + 1 < steps) step(i + 1, pb);
     }
+    if (ST && st) {
+        if constexpr (C == 2) { st[0] = z0.x; st[1] = z0.y; st[2] = z1.x; st[3] = z1.y; }
+        else { st[0] = z0; st[1] = z1; }
+    }
 }
 
 constexpr int FIR_THREADS = 256;
@@ -153,7 +169,8 @@ __global__ __launch_bounds__(FIR_THREADS) void k_fir(XmhFxJob j)
     for (int i = threadIdx.x; i < K; i += FIR_THREADS) h[i] = j.fir[K - 1 - i];
     for (int i = threadIdx.x; i < span * C; i += FIR_THREADS) {
         const int64_t f = jlo + i / C;
-        tile[i] = f >= 0 ? x[f * C + i % C] : 0.0f;
+        tile[i] = f >= 0 ? x[f * C + i % C]
+                         : (j.hist_in ? j.hist_in[((int64_t)clip * (K - 1) + (K - 1 + f)) * C + i % C] : 0.0f);
     }
     __syncthreads();
     float acc[FIR_OPT][C];
@@ -177,6 +194,21 @@ __global__ __launch_bounds__(FIR_THREADS) void k_fir(XmhFxJob j)
         if (n >= n1) continue;
 #pragma unroll
         for (int c = 0; c < C; ++c) y[n * C + c] = acc[o][c];
+    }
+}
+
+// Streaming FIR: the K-1 frames that precede the next block, from the old
+// history and this block's input (run before the FIR so in == out is safe).
+template <int C>
+__global__ __launch_bounds__(256) void k_fir_hist(XmhFxJob j)
+{
+    const int K1 = j.fir_len - 1;
+    const int clip = blockIdx.y;
+    const float *x = j.in_ptrs[clip];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < K1 * C; i += gridDim.x * 256) {
+        const int64_t p = j.frames - K1 + i / C;     // block-relative frame
+        j.hist_out[(int64_t)clip * K1 * C + i] =
+            p >= 0 ? x[p * C + i % C] : j.hist_in[((int64_t)clip * K1 + K1 + p) * C + i % C];
     }
 }
 
@@ -213,7 +245,8 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
     if (j->n_clips == 0 || j->frames == 0) return 0;
     const int kpw = 64 / j->n_sos;
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    auto kern = j->channels == 1 ? k_biquad_lanes<1, 32> : k_biquad_lanes<2, 32>;
+    auto kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 32, true> : k_biquad_lanes<2, 32, true>)
+                         : (j->channels == 1 ? k_biquad_lanes<1, 32, false> : k_biquad_lanes<2, 32, false>);
     XmhFxJob jj = *j;
     if (const char *d = getenv("XM_FX_DEV")) jj.dev_flags = atoi(d);   // dev attribution knob
     hipLaunchKernelGGL(kern, grid, dim3(64), 0, (hipStream_t)stream, jj);
@@ -227,6 +260,13 @@ extern "C" int xmh_launch_fx_fir(const XmhFxJob *j, void *stream)
     if (lds > 160 * 1024) return -1003;
     dim3 grid((unsigned)((j->frames + FIR_CHUNK - 1) / FIR_CHUNK), (unsigned)j->n_clips);
     if (grid.x == 0) return 0;
+    if (j->hist_in && K > 1) {                        // streaming: next block's history first
+        if (!j->hist_out || j->hist_out == j->hist_in) return -22;
+        auto hk = j->channels == 1 ? k_fir_hist<1> : k_fir_hist<2>;
+        hipLaunchKernelGGL(hk, dim3((unsigned)((K - 1) * j->channels + 255) / 256, (unsigned)j->n_clips), 256, 0,
+                           (hipStream_t)stream, *j);
+        if (hipGetLastError() != hipSuccess) return -1001;
+    }
     auto kern = j->channels == 1 ? k_fir<1> : k_fir<2>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

@@ -6,6 +6,8 @@
 // SURVEY.md §8(a) a2/a3/a6/a7).  The headline 48k->44.1k stereo fp32 path has
 // its own kernel (xm_resample_fast.hip); this file is the reference-order
 // fallback every other configuration uses, and the s16 mixer (config 3).
+#include <stdio.h>
+#include <stdlib.h>
 #include "xm_device.h"
 
 namespace {
@@ -25,8 +27,9 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int L = j.rs.L, M = j.rs.M, T = j.rs.T, rm = j.rs.rm;
     const int b = blockIdx.y;
-    const int64_t m0 = (int64_t)blockIdx.x * GEN_CHUNK;
-    const int64_t m1 = min(m0 + GEN_CHUNK, (int64_t)j.frames_out);
+    const int64_t ob = j.out_base, ib = j.in_base;   // streaming windows (0 for whole clips)
+    const int64_t m0 = ob + (int64_t)blockIdx.x * GEN_CHUNK;   // absolute output frames
+    const int64_t m1 = min(m0 + GEN_CHUNK, ob + (int64_t)j.frames_out);
     const int64_t N = j.frames_in;
 
     float *H = lds;                                  // L*T
@@ -50,13 +53,13 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
             const int16_t *x = (const int16_t *)xm_track_ptr(j, b, tr, 2);
             for (int i = threadIdx.x; i < span * C; i += GEN_THREADS) {
                 int64_t f = jlo + i / C;
-                tile[i] = (f >= 0 && f < N) ? (float)x[f * C + i % C] : 0.0f;
+                tile[i] = (f >= 0 && f < N) ? (float)x[(f - ib) * C + i % C] : 0.0f;
             }
         } else {
             const float *x = (const float *)xm_track_ptr(j, b, tr, 4);
             for (int i = threadIdx.x; i < span * C; i += GEN_THREADS) {
                 int64_t f = jlo + i / C;
-                tile[i] = (f >= 0 && f < N) ? x[f * C + i % C] : 0.0f;
+                tile[i] = (f >= 0 && f < N) ? x[(f - ib) * C + i % C] : 0.0f;
             }
         }
         __syncthreads();
@@ -96,15 +99,15 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
         if (S16 && PART) {
             int32_t *y = (int32_t *)xm_out_ptr(j, b, 4);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[m * C + c] = acci[o][c];
+            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = acci[o][c];
         } else if (S16) {
             int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[m * C + c] = xm_sat16(acci[o][c]);
+            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = xm_sat16(acci[o][c]);
         } else {
             float *y = (float *)xm_out_ptr(j, b, 4);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[m * C + c] = accf[o][c] + 0.0f;  // -0 -> +0 (scipy acc starts at +0)
+            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = accf[o][c] + 0.0f;  // -0 -> +0 (scipy acc starts at +0)
         }
     }
 }
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_s16(XmhMixJob j)
     const int64_t total = j.frames_out * C;
     const int64_t s0 = ((int64_t)blockIdx.x * MIX_THREADS + threadIdx.x) * SPT;
     if (s0 >= total) return;
-    const int64_t f0 = s0 / C;
+    const int64_t f0 = s0 / C + j.out_base;   // absolute frame (gain ramps)
     const bool full = s0 + SPT <= total;
 
     int32_t acc[SPT];
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_f32(XmhMixJob j)
     const int64_t total = j.frames_out * C;
     const int64_t s0 = ((int64_t)blockIdx.x * MIX_THREADS + threadIdx.x) * SPT;
     if (s0 >= total) return;
-    const int64_t f0 = s0 / C;
+    const int64_t f0 = s0 / C + j.out_base;   // absolute frame (gain ramps)
     const bool full = s0 + SPT <= total;
     float acc[SPT];
 #pragma unroll
@@ -275,7 +278,9 @@ int launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const XmhMi
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return -1001;
     hipLaunchKernelGGL(kern, grid, block, lds, s, j);
-    return hipGetLastError() == hipSuccess ? 0 : -1001;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess && getenv("XM_DEBUG")) fprintf(stderr, "generic launch: %s\n", hipGetErrorString(e));
+    return e == hipSuccess ? 0 : -1001;
 }
 
 }  // namespace

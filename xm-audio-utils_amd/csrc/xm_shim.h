@@ -66,6 +66,11 @@ typedef struct XmhMixJob {
     int32_t reserved2;
     void *scratch;            /* device scratch for staged paths */
     size_t scratch_bytes;
+    /* streaming windows (xm_audio_mixer_stream_*; 0 for whole clips):
+     * output row i of this launch is absolute output frame out_base + i (the
+     * gain ramps see the absolute frame); input row r is absolute input frame
+     * in_base + r; absolute frames outside [0, frames_in) read as zero. */
+    int64_t in_base, out_base;
 } XmhMixJob;
 
 /* ---------- effects job ---------------------------------------------------- */
@@ -81,6 +86,15 @@ typedef struct XmhFxJob {
     const float *fir;              /* device fir_len taps */
     int32_t dev_flags;             /* dev/attribution only (XM_FX_DEV env), 0 in the product */
     int32_t reserved;
+    /* streaming state (xm_effects_process_stream; NULL for whole clips):
+     * biquad: state[clip][section][z0,z1][channel], read at the start of the
+     *         block and written back after its last frame;
+     * FIR:    hist_in[clip][K-1][channel] = the K-1 frames before this block
+     *         (replace the zero left padding); hist_out gets the K-1 frames
+     *         before the next block (hist_out != hist_in). */
+    float *state;
+    const float *hist_in;
+    float *hist_out;
 } XmhFxJob;
 
 /* ---------- runtime --------------------------------------------------------- */
@@ -97,6 +111,8 @@ int  xmh_memcpy_h2d(void *dst, const void *src, size_t bytes, void *s);
 int  xmh_memcpy_d2h(void *dst, const void *src, size_t bytes, void *s);
 int  xmh_memcpy_d2d(void *dst, const void *src, size_t bytes, void *s);
 int  xmh_memset(void *dst, int v, size_t bytes, void *s);
+/* 2-D copy, any direction (hipMemcpyDefault): height rows of width bytes */
+int  xmh_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height, void *s);
 int  xmh_event_create(void **e);
 void xmh_event_destroy(void *e);
 int  xmh_event_record(void *e, void *s);

@@ -1,3 +1,5 @@
+#include <stdio.h>
+#include <stdlib.h>
 // xm_shim.hip — the thin C-ABI shim (SURVEY.md §1 layer L1): HIP runtime
 // wrappers with every hipError_t mapped to an XM_* status, and the kernel
 // dispatch for mix / effects jobs.  Only the C host layer (src/*.c) calls it.
@@ -9,9 +11,12 @@
 #define XM_ENOMEM_ (-12)
 #define XM_ENOSYS_ (-1003)
 
-static inline int map(hipError_t e)
+#define map(e) map_at((e), __LINE__)
+static inline int map_at(hipError_t e, int line)
 {
     if (e == hipSuccess) return 0;
+    if (getenv("XM_DEBUG")) fprintf(stderr, "xm_shim.hip:%d: %s\n", line, hipGetErrorString(e));
+    (void)hipGetLastError();   // reported through the return code: do not leave it for a later launch check
     if (e == hipErrorOutOfMemory) return XM_ENOMEM_;
     return XM_EDEVICE_;
 }
@@ -83,6 +88,12 @@ int xmh_memcpy_d2h(void *dst, const void *src, size_t n, void *s)
 int xmh_memcpy_d2d(void *dst, const void *src, size_t n, void *s)
 {
     return n ? map(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)s)) : 0;
+}
+
+int xmh_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height, void *s)
+{
+    if (!width || !height) return 0;
+    return map(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDefault, (hipStream_t)s));
 }
 
 int xmh_memset(void *dst, int v, size_t n, void *s)

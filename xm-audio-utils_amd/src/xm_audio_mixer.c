@@ -33,6 +33,13 @@ struct XmAudioMixer {
     size_t d_ptrs_cap;
     void **h_ptrs;                 /* pinned staging for the pointer table */
     const XmEffects *fx;
+    /* streaming (xm_audio_mixer_stream_*): window rows [batch*n_tracks] of
+     * st_cap frames, ping-pong st_win[st_cur]; row 0 holds absolute input
+     * frame st_w0, rows hold st_recv - st_w0 valid frames */
+    int st_on, st_ntr, st_cur;
+    size_t st_batch, st_cap;
+    int64_t st_recv, st_out, st_w0;
+    void *st_win[2];
 };
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
@@ -102,6 +109,8 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
     xmh_free(m->d_in);
     xmh_free(m->d_out);
     xmh_free(m->d_fx);
+    xmh_free(m->st_win[0]);
+    xmh_free(m->st_win[1]);
     xmh_free(m->d_ptrs);
     xmh_host_free(m->h_ptrs);
     for (int i = 0; i < 6; ++i) xmh_event_destroy(m->ev[i]);
@@ -555,4 +564,157 @@ int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in
     j.out_mix_stride = out_mix_stride;
     rc = run_job(m, &j);
     return finish(m, rc);
+}
+
+/* ---- streaming (build-owned) ----------------------
+ * Output m of the whole-signal resample reads input frames up to
+ * floor((m+rm)*M/L) and from floor((m+rm)*M/L) - T + 1 (xm_audio_common.h).
+ * After R frames have arrived every m < ceil(L*R/M) - rm is final; the flush
+ * (R = N) emits the rest up to ceil(N*L/M), frames >= N reading zero.  The
+ * device window keeps the input frames the next output still needs; each
+ * output is computed by the same kernel, taps and absolute gain index as in
+ * one whole-signal call, so the concatenated blocks equal it bit for bit. */
+static int64_t st_ready_out(const XmAudioMixer *m, int64_t R, int flush)
+{
+    const int64_t L = m->table.d.L, M = m->table.d.M, rm = m->table.d.rm;
+    if (flush) return (int64_t)xm_audio_mixer_out_frames(m, (size_t)R);
+    if (L == M) return R;
+    int64_t e = (L * R + M - 1) / M - rm;
+    return e > 0 ? e : 0;
+}
+
+static int64_t st_first_needed(const XmAudioMixer *m, int64_t mo)
+{
+    const int64_t L = m->table.d.L, M = m->table.d.M, rm = m->table.d.rm, T = m->table.d.T;
+    if (L == M) return mo;
+    return ((mo + rm) * M) / L - T + 1;
+}
+
+int xm_audio_mixer_stream_begin(XmAudioMixer *m, size_t batch)
+{
+    if (!m || batch == 0 || batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    if (m->fx) return XM_ENOSYS;   /* per-track effects: stream them with xm_effects_process_stream */
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    if ((rc = xmh_stream_sync(m->stream))) return rc;   /* a previous stream's copies */
+    m->st_on = 1;
+    m->st_ntr = m->n_tracks;
+    m->st_batch = batch;
+    m->st_recv = m->st_out = m->st_w0 = 0;
+    return XM_OK;
+}
+
+size_t xm_audio_mixer_stream_out_frames(const XmAudioMixer *m, size_t frames_in, int flush)
+{
+    if (!m || !m->st_on) return 0;
+    int64_t e = st_ready_out(m, m->st_recv + (int64_t)frames_in, flush);
+    return e > m->st_out ? (size_t)(e - m->st_out) : 0;
+}
+
+static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, size_t n, void *out,
+                   ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush)
+{
+    if (frames_out) *frames_out = 0;
+    if (!m || !m->st_on || (n && !in) || !frames_out) return XM_EINVAL;
+    if (m->fx) return XM_ENOSYS;
+    if (m->n_tracks != m->st_ntr) return XM_EINVAL;   /* track list changed mid-stream */
+    const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->st_ntr;
+    const size_t batch = m->st_batch, rows = batch * (size_t)ntr, fb = (size_t)C * (size_t)elem;
+    const int64_t R = m->st_recv + (int64_t)n;
+    int64_t mend = st_ready_out(m, R, flush);
+    if (mend < m->st_out) mend = m->st_out;
+    const size_t nout = (size_t)(mend - m->st_out);
+    if (nout && (!out || out_cap < nout)) return XM_EINVAL;
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    memset(&m->timing, 0, sizeof m->timing);
+    if ((rc = upload_gains(m))) return rc;
+    /* 1) append the block to the window */
+    const size_t keep = (size_t)(m->st_recv - m->st_w0);
+    if (keep + n > m->st_cap) {
+        size_t cap = keep + n + (keep + n) / 4 + 64;
+        void *nw[2] = {NULL, NULL};
+        rc = xmh_malloc(&nw[0], rows * cap * fb);
+        if (!rc) rc = xmh_malloc(&nw[1], rows * cap * fb);
+        if (!rc && keep)
+            rc = xmh_memcpy2d(nw[0], cap * fb, m->st_win[m->st_cur], m->st_cap * fb, keep * fb, rows, m->stream);
+        if (!rc) rc = xmh_stream_sync(m->stream);
+        if (rc) {
+            xmh_free(nw[0]);
+            xmh_free(nw[1]);
+            return rc;
+        }
+        xmh_free(m->st_win[0]);
+        xmh_free(m->st_win[1]);
+        m->st_win[0] = nw[0];
+        m->st_win[1] = nw[1];
+        m->st_cur = 0;
+        m->st_cap = cap;
+    }
+    char *win = (char *)m->st_win[m->st_cur];
+    const size_t pitch = m->st_cap * fb;
+    if (n) {
+        if (ms == (ptrdiff_t)ntr * ts || batch == 1)
+            rc = xmh_memcpy2d(win + keep * fb, pitch, in, (size_t)ts * (size_t)elem, n * fb, rows, m->stream);
+        else
+            for (size_t b = 0; !rc && b < batch; ++b)
+                rc = xmh_memcpy2d(win + (b * (size_t)ntr * pitch) + keep * fb, pitch,
+                                  (const char *)in + (ptrdiff_t)b * ms * elem, (size_t)ts * (size_t)elem, n * fb,
+                                  (size_t)ntr, m->stream);
+        if (rc) return rc;
+    }
+    m->st_recv = R;
+    /* 2) the outputs that are now final */
+    if (nout) {
+        int host = m->cfg.mem_kind != XM_MEM_DEVICE;
+        if (host && (rc = grow(&m->d_out, &m->d_out_cap, batch * nout * fb + 16))) return rc;
+        XmhMixJob j;
+        job_init(m, &j, batch, (size_t)R);
+        j.frames_out = (int64_t)nout;
+        j.in = win;
+        j.in_track_stride = (int64_t)(m->st_cap * (size_t)C);
+        j.in_mix_stride = j.in_track_stride * ntr;
+        j.in_base = m->st_w0;
+        j.out_base = m->st_out;
+        j.rs.fast = 0;
+        j.out = host ? m->d_out : out;
+        j.out_mix_stride = host ? (int64_t)(nout * (size_t)C) : (int64_t)os;
+        rc = run_job(m, &j);
+        if (!rc && host)
+            rc = xmh_memcpy2d(out, (size_t)os * (size_t)elem, m->d_out, nout * fb, nout * fb, batch, m->stream);
+        if (rc) return rc;
+    }
+    if (m->cfg.mem_kind != XM_MEM_DEVICE) {   /* host buffers are the caller's again on return */
+        if ((rc = xmh_stream_sync(m->stream))) return rc;
+    }
+    m->st_out = mend;
+    /* 3) drop the frames no later output reads (move the rest to the other buffer) */
+    int64_t w0 = st_first_needed(m, mend);
+    if (w0 > R) w0 = R;
+    if (w0 > m->st_w0 && !flush) {
+        const size_t left = (size_t)(R - w0);
+        if (left)
+            rc = xmh_memcpy2d(m->st_win[m->st_cur ^ 1], pitch, win + (size_t)(w0 - m->st_w0) * fb, pitch,
+                              left * fb, rows, m->stream);
+        if (rc) return rc;
+        m->st_cur ^= 1;
+        m->st_w0 = w0;
+    }
+    *frames_out = nout;
+    if (flush) m->st_on = 0;
+    if (!nout) return m->cfg.mem_kind == XM_MEM_DEVICE || m->user_stream ? XM_OK : xmh_stream_sync(m->stream);
+    return finish(m, rc);
+}
+
+int xm_audio_mixer_stream_push(XmAudioMixer *m, const void *in, ptrdiff_t in_track_stride, ptrdiff_t in_mix_stride,
+                               size_t frames_in, void *out, ptrdiff_t out_mix_stride, size_t out_cap,
+                               size_t *frames_out)
+{
+    return st_step(m, in, in_track_stride, in_mix_stride, frames_in, out, out_mix_stride, out_cap, frames_out, 0);
+}
+
+int xm_audio_mixer_stream_flush(XmAudioMixer *m, void *out, ptrdiff_t out_mix_stride, size_t out_cap,
+                                size_t *frames_out)
+{
+    return st_step(m, NULL, 0, 0, 0, out, out_mix_stride, out_cap, frames_out, 1);
 }

@@ -29,6 +29,13 @@ struct XmEffects {
     void **d_ptrs;
     void **h_ptrs;
     size_t ptr_cap;
+    /* streaming state (xm_effects_stream_reset): per stage, biquad
+     * [clip][section][z0,z1][ch] in st[s][0]; FIR [clip][K-1][ch] history
+     * ping-ponging between st[s][0] and st[s][1] (st_cur[s] = current) */
+    float *st[XM_MAX_EFFECTS][2];
+    int st_cur[XM_MAX_EFFECTS];
+    size_t st_clips;
+    int st_ready;
 };
 
 XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status)
@@ -66,10 +73,22 @@ XmEffects *xm_effects_create(int rate, int channels, int n_devices)
     return xm_effects_create_ex(&c, NULL);
 }
 
+static void free_stream_state(XmEffects *e)
+{
+    for (int i = 0; i < XM_MAX_EFFECTS; ++i)
+        for (int k = 0; k < 2; ++k) {
+            xmh_free(e->st[i][k]);
+            e->st[i][k] = NULL;
+        }
+    e->st_ready = 0;
+    e->st_clips = 0;
+}
+
 static void free_stages(XmEffects *e)
 {
     for (int i = 0; i < e->n_stages; ++i) xmh_free(e->stages[i].coef_dev);
     e->n_stages = 0;
+    free_stream_state(e);   /* streams belong to the chain they were started on */
 }
 
 void xm_effects_freep(XmEffects **pe)
@@ -79,6 +98,7 @@ void xm_effects_freep(XmEffects **pe)
     xmh_set_device(e->cfg.device);
     if (e->own_stream) xmh_stream_sync(e->own_stream);
     free_stages(e);
+    free_stream_state(e);
     for (int i = 0; i < e->n_effects; ++i) free(e->fx[i].fir);
     xmh_free(e->d_buf[0]);
     xmh_free(e->d_buf[1]);
@@ -261,7 +281,8 @@ static int ensure_ptrs(XmEffects *e, size_t n)
 
 /* Runs every stage; ping-pong through two device buffers so FIR never reads
  * what it writes.  src/dst: device pointer tables (n clips each). */
-static int run_chain(XmEffects *e, size_t batch, size_t frames, float **src, float **dst)
+static int run_chain(XmEffects *e, size_t batch, size_t frames, float **src, float **dst, int streaming,
+                     size_t clip0)
 {
     const int C = e->cfg.channels;
     const size_t per = frames * (size_t)C;
@@ -309,12 +330,19 @@ static int run_chain(XmEffects *e, size_t batch, size_t frames, float **src, flo
         j.frames = (int64_t)frames;
         j.in_ptrs = (const float *const *)cur;
         j.out_ptrs = (float *const *)nxt;
+        const size_t C2 = (size_t)C;
         if (e->stages[s].kind == 1) {
             j.sos = e->stages[s].coef_dev;
             j.n_sos = e->stages[s].n;
+            if (streaming) j.state = e->st[s][0] + clip0 * (size_t)j.n_sos * 2 * C2;
         } else {
             j.fir = e->stages[s].coef_dev;
             j.fir_len = e->stages[s].n;
+            if (streaming && j.fir_len > 1) {
+                const size_t off = clip0 * (size_t)(j.fir_len - 1) * C2;
+                j.hist_in = e->st[s][e->st_cur[s]] + off;
+                j.hist_out = e->st[s][e->st_cur[s] ^ 1] + off;
+            }
         }
         rc = xmh_launch_fx(&j, e->stream, &launches);
         cur = nxt;
@@ -322,14 +350,10 @@ static int run_chain(XmEffects *e, size_t batch, size_t frames, float **src, flo
     return rc;
 }
 
-int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const *out, size_t batch, size_t frames)
+static int process(XmEffects *e, const float *const *in, float *const *out, size_t batch, size_t frames,
+                   int streaming)
 {
-    if (!e || (batch && (!in || !out))) return XM_EINVAL;
-    if (batch == 0 || frames == 0) return XM_OK;
-    if (batch > (size_t)INT32_MAX / 2) return XM_EINVAL;
-    int rc = xmh_set_device(e->cfg.device);
-    if (!rc) rc = build_stages(e);
-    if (rc) return rc;
+    int rc = XM_OK;
     const size_t bytes = frames * (size_t)e->cfg.channels * sizeof(float);
     if (e->cfg.mem_kind == XM_MEM_DEVICE) {
         /* FIR stages must not run in place: route through scratch when in == out */
@@ -339,7 +363,7 @@ int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const 
             src[i] = (float *)in[i];
             dst[i] = out[i];
         }
-        if (!rc) rc = run_chain(e, batch, frames, src, dst);
+        if (!rc) rc = run_chain(e, batch, frames, src, dst, streaming, 0);
         free(src);
         free(dst);
     } else {
@@ -358,7 +382,7 @@ int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const 
                 dst[i] = (float *)d_io + (chunk + i) * (bytes / sizeof(float));
                 rc = xmh_memcpy_h2d(src[i], in[b0 + i], bytes, e->stream);
             }
-            if (!rc) rc = run_chain(e, nb, frames, src, dst);
+            if (!rc) rc = run_chain(e, nb, frames, src, dst, streaming, b0);
             for (size_t i = 0; !rc && i < nb; ++i) rc = xmh_memcpy_d2h(out[b0 + i], dst[i], bytes, e->stream);
             if (!rc) rc = xmh_stream_sync(e->stream);
         }
@@ -368,5 +392,63 @@ int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const 
         xmh_free(d_io);
     }
     if (!rc && !e->user_stream) rc = xmh_stream_sync(e->stream);
+    return rc;
+}
+
+int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const *out, size_t batch, size_t frames)
+{
+    if (!e || (batch && (!in || !out))) return XM_EINVAL;
+    if (batch == 0 || frames == 0) return XM_OK;
+    if (batch > (size_t)INT32_MAX / 2) return XM_EINVAL;
+    int rc = xmh_set_device(e->cfg.device);
+    if (!rc) rc = build_stages(e);
+    if (rc) return rc;
+    return process(e, in, out, batch, frames, 0);
+}
+
+/* ---- streaming ---------------------------------- */
+int xm_effects_stream_reset(XmEffects *e, size_t n_clips)
+{
+    if (!e || n_clips == 0 || n_clips > (size_t)INT32_MAX / 2) return XM_EINVAL;
+    int rc = xmh_set_device(e->cfg.device);
+    if (!rc) rc = build_stages(e);
+    if (rc) return rc;
+    xmh_stream_sync(e->stream);   /* a previous block may still use the old state */
+    free_stream_state(e);
+    const size_t C = (size_t)e->cfg.channels;
+    for (int s = 0; !rc && s < e->n_stages; ++s) {
+        const size_t per = e->stages[s].kind == 1 ? (size_t)e->stages[s].n * 2 * C
+                                                   : (size_t)(e->stages[s].n - 1) * C;
+        if (per == 0) continue;   /* 1-tap FIR: no history */
+        const size_t bytes = n_clips * per * sizeof(float);
+        const int nbuf = e->stages[s].kind == 1 ? 1 : 2;
+        for (int k = 0; !rc && k < nbuf; ++k) {
+            rc = xmh_malloc((void **)&e->st[s][k], bytes);
+            if (!rc) rc = xmh_memset(e->st[s][k], 0, bytes, e->stream);
+        }
+        e->st_cur[s] = 0;
+    }
+    if (!rc) rc = xmh_stream_sync(e->stream);
+    if (rc) {
+        free_stream_state(e);
+        return rc;
+    }
+    e->st_clips = n_clips;
+    e->st_ready = 1;
+    return XM_OK;
+}
+
+int xm_effects_process_stream(XmEffects *e, const float *const *in, float *const *out, size_t n_clips,
+                              size_t frames)
+{
+    if (!e || (n_clips && (!in || !out))) return XM_EINVAL;
+    if (e->dirty || !e->st_ready || n_clips != e->st_clips) return XM_EINVAL;   /* reset first */
+    if (frames == 0) return XM_OK;
+    int rc = xmh_set_device(e->cfg.device);
+    if (rc) return rc;
+    rc = process(e, in, out, n_clips, frames, 1);
+    if (!rc)
+        for (int s = 0; s < e->n_stages; ++s)
+            if (e->stages[s].kind == 2) e->st_cur[s] ^= 1;   /* hist_out becomes the history */
     return rc;
 }

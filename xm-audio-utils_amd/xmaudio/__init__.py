@@ -56,6 +56,8 @@ EXPORTED = [
     "xm_effects_create_ex", "xm_effects_create", "xm_effects_add_biquad", "xm_effects_add_eq_band",
     "xm_effects_add_fir", "xm_effects_count", "xm_effects_get_biquad", "xm_effects_set_stream",
     "xm_effects_process_batch", "xm_effects_freep",
+    "xm_audio_mixer_stream_begin", "xm_audio_mixer_stream_out_frames", "xm_audio_mixer_stream_push",
+    "xm_audio_mixer_stream_flush", "xm_effects_stream_reset", "xm_effects_process_stream",
 ]
 
 
@@ -116,6 +118,13 @@ _sigs = {
     "xm_effects_set_stream": (_i, [_vp, _vp]),
     "xm_effects_process_batch": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), _sz, _sz]),
     "xm_effects_freep": (None, [C.POINTER(_vp)]),
+    "xm_audio_mixer_stream_begin": (_i, [_vp, _sz]),
+    "xm_audio_mixer_stream_out_frames": (_sz, [_vp, _sz, _i]),
+    "xm_audio_mixer_stream_push": (_i, [_vp, _vp, C.c_ssize_t, C.c_ssize_t, _sz, _vp, C.c_ssize_t, _sz,
+                                        C.POINTER(_sz)]),
+    "xm_audio_mixer_stream_flush": (_i, [_vp, _vp, C.c_ssize_t, _sz, C.POINTER(_sz)]),
+    "xm_effects_stream_reset": (_i, [_vp, _sz]),
+    "xm_effects_process_stream": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), _sz, _sz]),
 }
 for _n, (_r, _a) in _sigs.items():
     _f = getattr(_lib, _n)
@@ -252,6 +261,52 @@ class Mixer:
         outs = (C.c_void_p * len(out_ptrs))(*out_ptrs)
         _check(_lib.xm_audio_mixer_process_batch(self._h, ins, outs, batch, frames_in), "process_batch")
 
+    # ---- streaming (xm_audio_mixer_stream_*; host memory mirror) ----
+    def stream_begin(self, batch: int):
+        _check(_lib.xm_audio_mixer_stream_begin(self._h, batch), "stream_begin")
+        self._st_batch = batch
+
+    def stream_out_frames(self, frames_in: int, flush: bool = False) -> int:
+        return _lib.xm_audio_mixer_stream_out_frames(self._h, frames_in, int(flush))
+
+    def stream_push(self, x: np.ndarray) -> np.ndarray:
+        """Host memory: block x [batch, n_tracks, frames, channels] -> the final output frames
+        [batch, n, channels] it releases."""
+        x = np.ascontiguousarray(x, self.dtype)
+        B, ntr, N, Cc = x.shape
+        assert B == self._st_batch and ntr == self.n_tracks and Cc == self.channels, x.shape
+        n = self.stream_out_frames(N)
+        y = np.empty((B, max(n, 1), Cc), self.dtype)
+        got = C.c_size_t(0)
+        _check(_lib.xm_audio_mixer_stream_push(self._h, x.ctypes.data if x.size else None, N * Cc, ntr * N * Cc,
+                                               N, y.ctypes.data, y.shape[1] * Cc, y.shape[1], C.byref(got)),
+               "stream_push")
+        assert got.value == n, (got.value, n)
+        return y[:, :n]
+
+    def stream_push_strided(self, in_ptr, in_track_stride: int, in_mix_stride: int, frames_in: int,
+                            out_ptr, out_mix_stride: int, out_cap: int) -> int:
+        """Any memory kind, caller layout (strides in elements); returns the frames written per mix."""
+        got = C.c_size_t(0)
+        _check(_lib.xm_audio_mixer_stream_push(self._h, in_ptr, in_track_stride, in_mix_stride, frames_in,
+                                               out_ptr, out_mix_stride, out_cap, C.byref(got)), "stream_push")
+        return got.value
+
+    def stream_flush_strided(self, out_ptr, out_mix_stride: int, out_cap: int) -> int:
+        got = C.c_size_t(0)
+        _check(_lib.xm_audio_mixer_stream_flush(self._h, out_ptr, out_mix_stride, out_cap, C.byref(got)),
+               "stream_flush")
+        return got.value
+
+    def stream_flush(self) -> np.ndarray:
+        n = self.stream_out_frames(0, True)
+        y = np.empty((self._st_batch, max(n, 1), self.channels), self.dtype)
+        got = C.c_size_t(0)
+        _check(_lib.xm_audio_mixer_stream_flush(self._h, y.ctypes.data, y.shape[1] * self.channels, y.shape[1],
+                                                C.byref(got)), "stream_flush")
+        assert got.value == n, (got.value, n)
+        return y[:, :n]
+
     def process_strided(self, in_ptr: int, in_track_stride: int, in_mix_stride: int, out_ptr: int,
                         out_mix_stride: int, batch: int, frames_in: int):
         _check(_lib.xm_audio_mixer_process_strided(self._h, in_ptr, in_track_stride, in_mix_stride, out_ptr,
@@ -329,3 +384,18 @@ class Effects:
         ins = (C.c_void_p * len(in_ptrs))(*in_ptrs)
         outs = (C.c_void_p * len(out_ptrs))(*out_ptrs)
         _check(_lib.xm_effects_process_batch(self._h, ins, outs, len(in_ptrs), frames), "effects_process_batch")
+
+    # ---- streaming (xm_effects_stream_reset / process_stream) ----
+    def stream_reset(self, n_clips: int):
+        _check(_lib.xm_effects_stream_reset(self._h, n_clips), "effects_stream_reset")
+
+    def process_stream(self, x: np.ndarray, inplace: bool = False) -> np.ndarray:
+        """Host memory: the next block x [n_clips, frames, channels] float32 of every stream."""
+        x = np.ascontiguousarray(x, np.float32)
+        B, N, Cc = x.shape
+        y = x if inplace else np.empty_like(x)
+        st = N * Cc * 4
+        ins = (C.c_void_p * B)(*[x.ctypes.data + i * st for i in range(B)])
+        outs = (C.c_void_p * B)(*[y.ctypes.data + i * st for i in range(B)])
+        _check(_lib.xm_effects_process_stream(self._h, ins, outs, B, N), "effects_process_stream")
+        return y
