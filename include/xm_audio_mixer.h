@@ -43,7 +43,9 @@ typedef struct XmMixerConfig {
 
 typedef struct XmTrackDesc {
     XmGainRamp gain;      /* per-track gain ramp / crossfade side */
-    int32_t    in_rate;   /* 0 = XmMixerConfig.in_rate; other values: XM_ENOSYS */
+    int32_t    in_rate;   /* 0 = XmMixerConfig.in_rate; another rate is resampled on its own
+                             to out_rate (process_timeline only; the uniform-length calls
+                             return XM_ENOSYS while such a track is set) */
     int32_t    reserved;
 } XmTrackDesc;
 
@@ -145,6 +147,26 @@ XM_API int xm_audio_mixer_stream_push(XmAudioMixer *m, const void *in, ptrdiff_t
                                ptrdiff_t out_mix_stride, size_t out_cap, size_t *frames_out);
 XM_API int xm_audio_mixer_stream_flush(XmAudioMixer *m, void *out, ptrdiff_t out_mix_stride,
                                 size_t out_cap, size_t *frames_out);
+
+/* ---- timeline mixes (build-owned; SURVEY.md §8(f) items 2-3: BGM/voice
+ * layouts, BASELINE.json:11).  Every track has its own length and may have
+ * its own input rate (XmTrackDesc.in_rate); it is resampled on its own to
+ * out_rate (exactly as a 1-track process_* call would) and placed so that its
+ * first resampled frame lands on output frame `offset` (negative: the head
+ * is cut).  out[b] gets out_frames frames: out[m] = ordered track sum of
+ * gain_tr(m) * r_tr[m - offset_tr], r_tr = 0 outside its resampled length;
+ * frames no track covers are silence.  The same placement applies to every
+ * mix of the batch.  in: batch*n_tracks pointers (mix-major), out: batch
+ * pointers, of the configured XmMemKind (host memory is staged one mix at a
+ * time).  Not with per-track effects (XM_ENOSYS). */
+typedef struct XmTrackPlacement {
+    int64_t offset;       /* output frame of the track's first resampled frame */
+    int64_t frames_in;    /* input frames of this track, at its own rate */
+} XmTrackPlacement;
+
+XM_API int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in,
+                                    const XmTrackPlacement *place, void *const *out,
+                                    size_t batch, size_t out_frames);
 
 XM_API int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t);
 

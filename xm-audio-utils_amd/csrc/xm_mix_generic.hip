@@ -230,6 +230,65 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_f32(XmhMixJob j)
     }
 }
 
+// Timeline mix: track tr of mix b is an already
+// resampled signal placed at output frame place[tr].offset for place[tr].len
+// frames; out[m] = ordered sum of g_tr(m) * x_tr[m - offset] with x_tr = 0
+// outside [0, len).  A track that does not reach the thread's frames is
+// skipped: its terms are +-0, which leaves a non-zero acc unchanged and only
+// the sign of a zero acc, normalised by the final +0; Q15
+// terms of 0 are exactly 0.  Gains are evaluated at the mix's frame m.
+template <int C, bool S16>
+__global__ __launch_bounds__(MIX_THREADS) void k_mix_placed(XmhMixJob j)
+{
+    constexpr int SPT = S16 ? 8 : 4;       // 16 B of output per thread
+    constexpr int FPT = SPT / C;
+    const int b = blockIdx.y;
+    const int64_t total = j.frames_out * C;
+    const int64_t s0 = ((int64_t)blockIdx.x * MIX_THREADS + threadIdx.x) * SPT;
+    if (s0 >= total) return;
+    const int64_t f0 = s0 / C;
+    float accf[SPT];
+    int32_t acci[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) { accf[i] = 0.0f; acci[i] = 0; }
+    for (int tr = 0; tr < j.n_tracks; ++tr) {
+        const int64_t off = j.place[2 * tr], len = j.place[2 * tr + 1];
+        const int64_t lo = f0 - off;                 // track frame of the thread's first frame
+        if (lo + FPT <= 0 || lo >= len) continue;
+        const XmhGain g = j.gains[tr];
+        const void *xp = j.in_ptrs[(int64_t)b * j.n_tracks + tr];
+#pragma unroll
+        for (int f = 0; f < FPT; ++f) {
+            const int64_t tf = lo + f;
+            const bool in = tf >= 0 && tf < len && s0 + f * C < total;
+            if (S16) {
+                const int32_t gq = xm_gain_q15(g, f0 + f);
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int32_t v = in ? ((const int16_t *)xp)[tf * C + c] : 0;
+                    acci[f * C + c] += xm_q15_term(v, gq);
+                }
+            } else {
+                const float gf = xm_gain_f32(g, f0 + f);
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const float v = in ? ((const float *)xp)[tf * C + c] : 0.0f;
+                    accf[f * C + c] = accf[f * C + c] + gf * v;
+                }
+            }
+        }
+    }
+    if (S16) {
+        int16_t *y = (int16_t *)xm_out_ptr(j, b, 2) + s0;
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) y[i] = xm_sat16(acci[i]);
+    } else {
+        float *y = (float *)xm_out_ptr(j, b, 4) + s0;
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) y[i] = accf[i] + 0.0f;
+    }
+}
+
 // Config 5 finish: out = sat16(sum of n_parts int32 partials, in part order).
 // 8 samples (32 B of each partial, 16 B out) per thread, coalesced.
 __global__ __launch_bounds__(MIX_THREADS) void k_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride,
@@ -321,6 +380,22 @@ extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
                               : launch(k_resample_mix_generic<2, true>, grid, GEN_THREADS, lds, s, *j);
     else     rc = C == 1 ? launch(k_resample_mix_generic<1, false>, grid, GEN_THREADS, lds, s, *j)
                          : launch(k_resample_mix_generic<2, false>, grid, GEN_THREADS, lds, s, *j);
+    if (n_launches) *n_launches += 1;
+    return rc;
+}
+
+extern "C" int xmh_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
+{
+    if (j->frames_out == 0 || j->n_mix == 0) return 0;
+    if (!j->place || !j->in_ptrs || (j->channels != 1 && j->channels != 2)) return -22;
+    const bool s16 = j->fmt == 1;
+    const int64_t spt = s16 ? 8 : 4, samples = j->frames_out * j->channels;
+    dim3 grid((unsigned)((samples + MIX_THREADS * spt - 1) / (MIX_THREADS * spt)), (unsigned)j->n_mix);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = s16 ? (j->channels == 1 ? launch(k_mix_placed<1, true>, grid, MIX_THREADS, 0, s, *j)
+                                     : launch(k_mix_placed<2, true>, grid, MIX_THREADS, 0, s, *j))
+                 : (j->channels == 1 ? launch(k_mix_placed<1, false>, grid, MIX_THREADS, 0, s, *j)
+                                     : launch(k_mix_placed<2, false>, grid, MIX_THREADS, 0, s, *j));
     if (n_launches) *n_launches += 1;
     return rc;
 }

@@ -71,6 +71,9 @@ typedef struct XmhMixJob {
      * gain ramps see the absolute frame); input row r is absolute input frame
      * in_base + r; absolute frames outside [0, frames_in) read as zero. */
     int64_t in_base, out_base;
+    /* timeline mix (xmh_launch_mix_placed): device [n_tracks][2] int64 =
+     * (output frame of the track's first frame, track length in frames) */
+    const int64_t *place;
 } XmhMixJob;
 
 /* ---------- effects job ---------------------------------------------------- */
@@ -124,6 +127,10 @@ const char *xmh_arch_name(void);
 /* resample (if rs.L != rs.M) + gain + ordered track sum; returns launches made */
 int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches);
 int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
+/* timeline mix: out[m] = ordered sum over tracks of g_tr(m) * x_tr[m - place_tr.offset],
+ * x_tr zero outside [0, place_tr.len); in_ptrs[b*n_tracks+tr] are the (resampled)
+ * tracks, rs ignored */
+int xmh_launch_mix_placed(const XmhMixJob *job, void *stream, int *n_launches);
 /* config 5 finish: out[b][i] = sat16(sum over p of parts[p*part_stride + b*part_mix_stride + i]) */
 int xmh_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
                           int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream);

@@ -40,6 +40,14 @@ struct XmAudioMixer {
     size_t st_batch, st_cap;
     int64_t st_recv, st_out, st_w0;
     void *st_win[2];
+    /* per-track input rates (xm_audio_mixer_process_timeline): cached tables
+     * for rates other than cfg.in_rate; trk_rt[tr] = index, -1 = m->table */
+    XmTable rt[XM_MAX_TRACKS];
+    int32_t rt_rate[XM_MAX_TRACKS];
+    int n_rt, mixed_rates;
+    int trk_rt[XM_MAX_TRACKS];
+    int64_t *place_dev;            /* [XM_MAX_TRACKS][2] */
+    XmhGain *unity_dev;            /* one unity-gain descriptor */
 };
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
@@ -111,6 +119,9 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
     xmh_free(m->d_fx);
     xmh_free(m->st_win[0]);
     xmh_free(m->st_win[1]);
+    for (int i = 0; i < m->n_rt; ++i) xm_table_free(&m->rt[i]);
+    xmh_free(m->place_dev);
+    xmh_free(m->unity_dev);
     xmh_free(m->d_ptrs);
     xmh_host_free(m->h_ptrs);
     for (int i = 0; i < 6; ++i) xmh_event_destroy(m->ev[i]);
@@ -123,11 +134,28 @@ int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_
 {
     if (!m || !tracks || n_tracks < 1 || n_tracks > XM_MAX_TRACKS) return XM_EINVAL;
     XmhGain g[XM_MAX_TRACKS];
+    int trk_rt[XM_MAX_TRACKS], mixed = 0;
     for (int i = 0; i < n_tracks; ++i) {
-        if (tracks[i].in_rate != 0 && tracks[i].in_rate != m->cfg.in_rate) return XM_ENOSYS;
+        if (tracks[i].in_rate < 0) return XM_EINVAL;
         int rc = xm_gain_to_dev(&tracks[i].gain, &g[i]);
         if (rc) return rc;
+        trk_rt[i] = -1;
+        const int32_t r = tracks[i].in_rate;
+        if (r == 0 || r == m->cfg.in_rate) continue;
+        mixed = 1;
+        int k = 0;
+        while (k < m->n_rt && m->rt_rate[k] != r) ++k;
+        if (k == m->n_rt) {   /* a new rate: design its table once and keep it */
+            if (m->n_rt == XM_MAX_TRACKS) return XM_ENOMEM;
+            if ((rc = xmh_set_device(m->cfg.device))) return rc;
+            if ((rc = xm_table_build(&m->rt[k], r, m->cfg.out_rate))) return rc;
+            m->rt_rate[k] = r;
+            m->n_rt++;
+        }
+        trk_rt[i] = k;
     }
+    memcpy(m->trk_rt, trk_rt, sizeof(int) * (size_t)n_tracks);
+    m->mixed_rates = mixed;
     memcpy(m->tracks, tracks, sizeof(XmTrackDesc) * (size_t)n_tracks);
     memcpy(m->gains, g, sizeof(XmhGain) * (size_t)n_tracks);
     m->n_tracks = n_tracks;
@@ -462,6 +490,7 @@ static int process_host(XmAudioMixer *m, const void *const *in, void *const *out
 int xm_audio_mixer_process_batch(XmAudioMixer *m, const void *const *in, void *const *out, size_t batch,
                                  size_t frames_in)
 {
+    if (m && m->mixed_rates) return XM_ENOSYS;   /* tracks of other rates: process_timeline */
     if (!m || (batch && (!in || !out))) return XM_EINVAL;
     if (batch == 0) return XM_OK;
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
@@ -484,7 +513,8 @@ int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in, ptrdiff_
                                        size_t batch, size_t frames_in)
 {
     if (!m || (batch && (!in || !partial))) return XM_EINVAL;
-    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx) return XM_ENOSYS;
+    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx || m->mixed_rates)
+        return XM_ENOSYS;
     if (batch == 0) return XM_OK;
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
@@ -530,6 +560,7 @@ int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in
                                    ptrdiff_t in_mix_stride, void *out, ptrdiff_t out_mix_stride, size_t batch,
                                    size_t frames_in)
 {
+    if (m && m->mixed_rates) return XM_ENOSYS;   /* tracks of other rates: process_timeline */
     if (!m || (batch && (!in || !out))) return XM_EINVAL;
     if (batch == 0) return XM_OK;
     if (m->cfg.mem_kind != XM_MEM_DEVICE) {
@@ -593,7 +624,7 @@ static int64_t st_first_needed(const XmAudioMixer *m, int64_t mo)
 int xm_audio_mixer_stream_begin(XmAudioMixer *m, size_t batch)
 {
     if (!m || batch == 0 || batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
-    if (m->fx) return XM_ENOSYS;   /* per-track effects: stream them with xm_effects_process_stream */
+    if (m->fx || m->mixed_rates) return XM_ENOSYS;   /* effects: xm_effects_process_stream */
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
     if ((rc = xmh_stream_sync(m->stream))) return rc;   /* a previous stream's copies */
@@ -717,4 +748,139 @@ int xm_audio_mixer_stream_flush(XmAudioMixer *m, void *out, ptrdiff_t out_mix_st
                                 size_t *frames_out)
 {
     return st_step(m, NULL, 0, 0, 0, out, out_mix_stride, out_cap, frames_out, 1);
+}
+
+/* ---- timeline mixes (build-owned) ---------
+ * Each track is first resampled on its own (its XmTrackDesc.in_rate, same
+ * kernels and order as a 1-track unity-gain mix, which equals the fused
+ * per-track resample bit for bit: 0 + 1*r == r, and a Q15 unity term is the
+ * sample itself), then placed at its output-frame offset and mixed with the
+ * gains evaluated at the mix's output frame. */
+static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrackPlacement *place,
+                           void *const *out, size_t batch, size_t out_frames)
+{
+    const int ntr = m->n_tracks, C = m->cfg.channels, elem = fmt_bytes(m->cfg.sample_fmt);
+    int rc = XM_OK, launches = 0;
+    if (!m->place_dev && (rc = xmh_malloc((void **)&m->place_dev, sizeof(int64_t) * 2 * XM_MAX_TRACKS))) return rc;
+    if (!m->unity_dev) {
+        static const XmhGain ug = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
+        if ((rc = xmh_malloc((void **)&m->unity_dev, sizeof ug))) return rc;
+        if ((rc = xmh_memcpy_h2d(m->unity_dev, &ug, sizeof ug, m->stream))) return rc;
+    }
+    /* resampled lengths and scratch offsets */
+    int64_t pl[2 * XM_MAX_TRACKS];
+    size_t off[XM_MAX_TRACKS], scratch = 0;
+    for (int tr = 0; tr < ntr; ++tr) {
+        const XmTable *t = m->trk_rt[tr] < 0 ? &m->table : &m->rt[m->trk_rt[tr]];
+        const int64_t n = place[tr].frames_in;
+        pl[2 * tr] = place[tr].offset;
+        pl[2 * tr + 1] = t->d.L == t->d.M ? n : (n * t->d.L + t->d.M - 1) / t->d.M;
+        off[tr] = scratch;
+        if (t->d.L != t->d.M) scratch += batch * (size_t)pl[2 * tr + 1] * (size_t)C * (size_t)elem + 256;
+    }
+    if ((rc = grow(&m->d_fx, &m->d_fx_cap, scratch + 16))) return rc;
+    /* pointer table: [track-major inputs ntr*batch][mix-major placed tracks batch*ntr] + [batch outputs] */
+    const size_t nb = batch * (size_t)ntr;
+    const void **hp = malloc(sizeof(void *) * 2 * nb);
+    if (!hp) return XM_ENOMEM;
+    for (int tr = 0; tr < ntr; ++tr)
+        for (size_t b = 0; b < batch; ++b) {
+            const XmTable *t = m->trk_rt[tr] < 0 ? &m->table : &m->rt[m->trk_rt[tr]];
+            hp[(size_t)tr * batch + b] = in[b * (size_t)ntr + (size_t)tr];
+            hp[nb + b * (size_t)ntr + (size_t)tr] =
+                t->d.L == t->d.M ? in[b * (size_t)ntr + (size_t)tr]
+                                 : (const char *)m->d_fx + off[tr] + b * (size_t)pl[2 * tr + 1] * (size_t)C * (size_t)elem;
+        }
+    const void *const *din = NULL;
+    void *const *dout = NULL;
+    rc = ptr_table(m, hp, 2 * nb, out, batch, &din, &dout);
+    free(hp);
+    if (!rc) rc = xmh_memcpy_h2d(m->place_dev, pl, sizeof(int64_t) * 2 * (size_t)ntr, m->stream);
+    if (!rc) rc = xmh_event_record(m->ev[2], m->stream);
+    for (int tr = 0; !rc && tr < ntr; ++tr) {
+        const XmTable *t = m->trk_rt[tr] < 0 ? &m->table : &m->rt[m->trk_rt[tr]];
+        if (t->d.L == t->d.M || place[tr].frames_in == 0) continue;
+        XmhMixJob j;
+        memset(&j, 0, sizeof j);
+        j.fmt = m->cfg.sample_fmt;
+        j.channels = C;
+        j.n_tracks = 1;
+        j.n_mix = (int32_t)batch;
+        j.frames_in = place[tr].frames_in;
+        j.frames_out = pl[2 * tr + 1];
+        j.in_ptrs = din + (size_t)tr * batch;
+        j.out = (char *)m->d_fx + off[tr];
+        j.out_mix_stride = pl[2 * tr + 1] * C;
+        j.gains = m->unity_dev;
+        j.unity = 1;
+        j.rs.L = t->d.L;
+        j.rs.M = t->d.M;
+        j.rs.T = t->d.T;
+        j.rs.rm = t->d.rm;
+        j.rs.H = t->H_dev;
+        j.rs.fast = 0;
+        rc = xmh_launch_mix(&j, m->stream, &launches);
+    }
+    if (!rc) {
+        XmhMixJob j;
+        memset(&j, 0, sizeof j);
+        j.fmt = m->cfg.sample_fmt;
+        j.channels = C;
+        j.n_tracks = ntr;
+        j.n_mix = (int32_t)batch;
+        j.frames_out = (int64_t)out_frames;
+        j.in_ptrs = din + nb;
+        j.out_ptrs = dout;
+        j.gains = m->gains_dev;
+        j.place = m->place_dev;
+        rc = xmh_launch_mix_placed(&j, m->stream, &launches);
+    }
+    if (!rc) rc = xmh_event_record(m->ev[3], m->stream);
+    m->timing.n_launches += launches;
+    return rc;
+}
+
+int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, const XmTrackPlacement *place,
+                                    void *const *out, size_t batch, size_t out_frames)
+{
+    if (!m || !place || (batch && (!in || !out))) return XM_EINVAL;
+    if (m->fx) return XM_ENOSYS;
+    if (batch == 0 || out_frames == 0) return XM_OK;
+    if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    const int ntr = m->n_tracks;
+    for (int tr = 0; tr < ntr; ++tr)
+        if (place[tr].frames_in < 0 || place[tr].frames_in > ((int64_t)1 << 40)) return XM_EINVAL;
+    for (size_t i = 0; i < batch * (size_t)ntr; ++i)
+        if (!in[i]) return XM_EINVAL;
+    for (size_t i = 0; i < batch; ++i)
+        if (!out[i]) return XM_EINVAL;
+    int rc = xmh_set_device(m->cfg.device);
+    if (rc) return rc;
+    memset(&m->timing, 0, sizeof m->timing);
+    if ((rc = upload_gains(m))) return rc;
+    if (m->cfg.mem_kind == XM_MEM_DEVICE) return finish(m, timeline_device(m, in, place, out, batch, out_frames));
+    /* host memory: stage one mix at a time */
+    const int C = m->cfg.channels, elem = fmt_bytes(m->cfg.sample_fmt);
+    size_t in_bytes = 0, toff[XM_MAX_TRACKS];
+    for (int tr = 0; tr < ntr; ++tr) {
+        toff[tr] = in_bytes;
+        in_bytes += (size_t)place[tr].frames_in * (size_t)C * (size_t)elem + 256;
+    }
+    const size_t out_bytes = out_frames * (size_t)C * (size_t)elem;
+    rc = grow(&m->d_in, &m->d_in_cap, in_bytes + 16);
+    if (!rc) rc = grow(&m->d_out, &m->d_out_cap, out_bytes + 16);
+    const void *dp[XM_MAX_TRACKS];
+    void *dop[1];
+    for (size_t b = 0; !rc && b < batch; ++b) {
+        for (int tr = 0; !rc && tr < ntr; ++tr) {
+            dp[tr] = (char *)m->d_in + toff[tr];
+            rc = xmh_memcpy_h2d((void *)dp[tr], in[b * (size_t)ntr + (size_t)tr],
+                                (size_t)place[tr].frames_in * (size_t)C * (size_t)elem, m->stream);
+        }
+        dop[0] = m->d_out;
+        if (!rc) rc = timeline_device(m, dp, place, dop, 1, out_frames);
+        if (!rc) rc = xmh_memcpy_d2h(out[b], m->d_out, out_bytes, m->stream);
+        if (!rc) rc = xmh_stream_sync(m->stream);
+    }
+    return finish(m, rc);
 }

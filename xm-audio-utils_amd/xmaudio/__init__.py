@@ -58,6 +58,7 @@ EXPORTED = [
     "xm_effects_process_batch", "xm_effects_freep",
     "xm_audio_mixer_stream_begin", "xm_audio_mixer_stream_out_frames", "xm_audio_mixer_stream_push",
     "xm_audio_mixer_stream_flush", "xm_effects_stream_reset", "xm_effects_process_stream",
+    "xm_audio_mixer_process_timeline",
 ]
 
 
@@ -83,6 +84,10 @@ class XmMixerTiming(C.Structure):
 
 class XmEffectsConfig(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("rate", "channels", "mem_kind", "device")]
+
+
+class XmTrackPlacement(C.Structure):
+    _fields_ = [("offset", C.c_int64), ("frames_in", C.c_int64)]
 
 
 class XmResampleDesign(C.Structure):
@@ -124,6 +129,8 @@ _sigs = {
                                         C.POINTER(_sz)]),
     "xm_audio_mixer_stream_flush": (_i, [_vp, _vp, C.c_ssize_t, _sz, C.POINTER(_sz)]),
     "xm_effects_stream_reset": (_i, [_vp, _sz]),
+    "xm_audio_mixer_process_timeline": (_i, [_vp, C.POINTER(_vp), C.POINTER(XmTrackPlacement), C.POINTER(_vp),
+                                             _sz, _sz]),
     "xm_effects_process_stream": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), _sz, _sz]),
 }
 for _n, (_r, _a) in _sigs.items():
@@ -260,6 +267,20 @@ class Mixer:
         ins = (C.c_void_p * len(in_ptrs))(*in_ptrs)
         outs = (C.c_void_p * len(out_ptrs))(*out_ptrs)
         _check(_lib.xm_audio_mixer_process_batch(self._h, ins, outs, batch, frames_in), "process_batch")
+
+    def process_timeline(self, tracks, offsets, out_frames: int) -> np.ndarray:
+        """Host memory: tracks = one array [batch, frames_tr, channels] per track (own length,
+        own rate as set by set_tracks), offsets = output frame of each track's first frame."""
+        ts = [np.ascontiguousarray(t, self.dtype) for t in tracks]
+        assert len(ts) == self.n_tracks == len(offsets)
+        B = ts[0].shape[0]
+        y = np.empty((B, out_frames, self.channels), self.dtype)
+        ins = (C.c_void_p * (B * len(ts)))(*[t[b].ctypes.data if t.shape[1] else y.ctypes.data
+                                             for b in range(B) for t in ts])
+        pl = (XmTrackPlacement * len(ts))(*[XmTrackPlacement(int(o), t.shape[1]) for o, t in zip(offsets, ts)])
+        outs = (C.c_void_p * B)(*[y[b].ctypes.data for b in range(B)])
+        _check(_lib.xm_audio_mixer_process_timeline(self._h, ins, pl, outs, B, out_frames), "process_timeline")
+        return y
 
     # ---- streaming (xm_audio_mixer_stream_*; host memory mirror) ----
     def stream_begin(self, batch: int):
