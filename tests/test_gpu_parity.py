@@ -226,6 +226,27 @@ def test_mixer_with_track_eq_vs_c_oracle(xm, gpu):
     assert bits_equal(y, CO.mix_f32(r, ramps))
 
 
+def test_mixer_with_track_biquad_fir_chain(xm, gpu):
+    """Per-track chain with FIR stages (ping-pong track buffers): resample ->
+    biquad x2 -> FIR 63 -> biquad -> FIR 7 -> gain -> ordered mix."""
+    z = golden("effects.npz")
+    x = np.stack([O.gen_f32(SEED, 970 + t, 2, 9600 + 3) for t in range(3)])[None]
+    ramps = HEADLINE_RAMPS[:3]
+    e = xm.Effects(44100, 2)
+    e.add_biquad(z["sos"][0])
+    e.add_biquad(z["sos"][1])
+    e.add_fir(z["h63"])
+    e.add_biquad(z["sos"][2])
+    e.add_fir(z["h7"])
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(ramps)
+    m.set_track_effects(e)
+    y = m.process(x)[0]
+    r = [CO.fir_f32(CO.biquad_f32(CO.fir_f32(CO.biquad_f32(CO.resample_f32(t, 147, 160), z["sos"][:2]), z["h63"]),
+                                  z["sos"][2:3]), z["h7"]) for t in x[0]]
+    assert bits_equal(y, CO.mix_f32(r, ramps))
+
+
 def test_device_memory_strided_and_ptrs(xm, gpu):
     """XM_MEM_DEVICE through torch-allocated HBM: strided, pointer tables and a
     caller stream all give the host-mode bits."""
@@ -278,8 +299,9 @@ def test_errors(xm, gpu):
     assert e.value.code == xm.XM_EINVAL
     with pytest.raises(xm.XmError):
         m.set_tracks([dict()] * 65)
+    m.set_tracks([dict(in_rate=22050)])   # another rate: only process_timeline takes it
     with pytest.raises(xm.XmError) as e:
-        m.set_tracks([dict(in_rate=22050)])
+        m.process(np.zeros((1, 1, 100, 2), np.float32))
     assert e.value.code == xm.XM_ENOSYS
     with pytest.raises(xm.XmError):
         xm.Mixer(48000, 44100, 2, "f32", device=99)

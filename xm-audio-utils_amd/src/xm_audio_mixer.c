@@ -258,9 +258,18 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     const int C = j0->channels, ntr = j0->n_tracks;
     const size_t per_track = (size_t)j0->frames_out * (size_t)C;
     const size_t ntot = (size_t)j0->n_mix * (size_t)ntr;
-    int rc = grow(&m->d_fx, &m->d_fx_cap, ntot * per_track * sizeof(float) + 256);
+    /* FIR stages read neighbours of what they write: they ping-pong between
+     * two track buffers; biquad cascades run in place */
+    const XmFxStage *st = NULL;
+    int ns = 0, has_fir = 0;
+    int rc = xm_effects_stages(m->fx, &st, &ns);
+    if (rc) return rc;
+    for (int s = 0; s < ns; ++s) has_fir |= st[s].kind == 2;
+    const size_t buf_bytes = (ntot * per_track * sizeof(float) + 255) & ~(size_t)255;
+    rc = grow(&m->d_fx, &m->d_fx_cap, buf_bytes * (has_fir ? 2 : 1) + 256);
     if (rc) return rc;
     float *scratch = (float *)m->d_fx;
+    float *scratch2 = (float *)((char *)m->d_fx + buf_bytes);
     /* 1) resample: treat every track as its own 1-track mix (unity gain) */
     static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
     XmhGain *ug = NULL;
@@ -285,18 +294,19 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         rc = XM_ENOSYS;   /* irregular strides with effects: use process_batch */
     }
     if (!rc) rc = xmh_launch_mix(&r, m->stream, launches);
-    /* 2) effects chain on every track, in insertion order, in place */
-    const XmFxStage *st = NULL;
-    int ns = 0;
-    if (!rc) rc = xm_effects_stages(m->fx, &st, &ns);
+    /* 2) effects chain on every track, in insertion order */
     void **tmp_ptrs = NULL;
+    int cur = 0;   /* 0: tracks in scratch, 1: in scratch2 */
     if (!rc && ns > 0) {
         rc = xmh_malloc((void **)&tmp_ptrs, sizeof(void *) * ntot * 2);
         void **hp = malloc(sizeof(void *) * ntot * 2);
         if (!hp) rc = XM_ENOMEM;
         if (!rc) {
-            for (size_t i = 0; i < ntot; ++i) hp[i] = scratch + i * per_track;
-            rc = xmh_memcpy_h2d(tmp_ptrs, hp, sizeof(void *) * ntot, m->stream);
+            for (size_t i = 0; i < ntot; ++i) {
+                hp[i] = scratch + i * per_track;
+                hp[ntot + i] = scratch2 + i * per_track;
+            }
+            rc = xmh_memcpy_h2d(tmp_ptrs, hp, sizeof(void *) * ntot * (has_fir ? 2 : 1), m->stream);
             if (!rc) rc = xmh_stream_sync(m->stream);
         }
         free(hp);
@@ -306,22 +316,24 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
             fj.channels = C;
             fj.n_clips = (int32_t)ntot;
             fj.frames = j0->frames_out;
-            fj.in_ptrs = (const float *const *)tmp_ptrs;
-            fj.out_ptrs = (float *const *)tmp_ptrs;
+            fj.in_ptrs = (const float *const *)(tmp_ptrs + (size_t)cur * ntot);
             if (st[s].kind == 1) {
+                fj.out_ptrs = (float *const *)(tmp_ptrs + (size_t)cur * ntot);
                 fj.sos = st[s].coef_dev;
                 fj.n_sos = st[s].n;
             } else {
-                rc = XM_ENOSYS;   /* FIR in-place needs a second buffer; biquad chains only */
-                break;
+                fj.out_ptrs = (float *const *)(tmp_ptrs + (size_t)(cur ^ 1) * ntot);
+                fj.fir = st[s].coef_dev;
+                fj.fir_len = st[s].n;
             }
             rc = xmh_launch_fx(&fj, m->stream, launches);
+            if (st[s].kind == 2) cur ^= 1;
         }
     }
     /* 3) mix, no resampling */
     if (!rc) {
         XmhMixJob x = *j0;
-        x.in = scratch;
+        x.in = cur ? scratch2 : scratch;
         x.in_ptrs = NULL;
         x.in_track_stride = (int64_t)per_track;
         x.in_mix_stride = (int64_t)(per_track * (size_t)ntr);
