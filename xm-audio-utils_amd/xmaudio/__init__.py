@@ -134,6 +134,8 @@ _sigs = {
     "xm_effects_process_stream": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), _sz, _sz]),
 }
 for _n, (_r, _a) in _sigs.items():
+    if os.environ.get("XM_AUDIO_LIB") and not hasattr(_lib, _n):
+        continue   # dev: an older ablation build lacks newer entry points
     _f = getattr(_lib, _n)
     _f.restype, _f.argtypes = _r, _a
 
