@@ -173,3 +173,22 @@ def test_effects_stream_errors(xm, gpu):
     e.stream_reset(3)
     with pytest.raises(xm.XmError):   # clip count differs from the reset
         e.process_stream(x)
+
+
+@pytest.mark.parametrize("knob", [("XM_BQ_CH", "32"), ("XM_BQ_SPLIT", "1")])
+def test_biquad_ab_variants_stay_exact(xm, gpu, monkeypatch, knob):
+    """The A/B kernel variants (32-frame chunks; one channel per lane) keep the
+    bits, whole-clip and streamed, so a later switch of default is safe."""
+    z = golden("effects.npz")
+    x = np.stack([O.gen_f32(SEED, 3500 + b, 2, 5000 + 3) for b in range(7)])
+    monkeypatch.setenv(*knob)
+    e = xm.Effects(48000, 2)
+    for s in z["sos"]:
+        e.add_biquad(s)
+    y = e.process(x)
+    e.stream_reset(7)
+    ys = np.concatenate([e.process_stream(x[:, :1001]), e.process_stream(x[:, 1001:1002]),
+                         e.process_stream(x[:, 1002:])], axis=1)
+    for b in range(7):
+        r = CO.biquad_f32(x[b], z["sos"])
+        assert bits_equal(y[b], r) and bits_equal(ys[b], r), b

@@ -148,6 +148,120 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
     }
 }
 
+// Stereo cascade with one channel per lane: lane = (clip k, channel ch,
+// section s) = (k*2 + ch)*NS + s, 64 / (2*NS) clips per wave.  Same chunked
+// section pipeline as k_biquad_lanes, but the recurrence runs on plain fp32
+// ops: a wave64 v_pk_*_f32 issues in ~4.3 clk per SIMD against ~2.4 clk for
+// v_mul/v_add_f32 (tools/ubench/valu_rate.hip), and a lane's per-frame
+// instruction stream (9 ops around a 4-op dependent chain) was expected to
+// bound the time.  Measured on config 4 it is slower (EQ 23.3 ms against 20.3
+// for packed lanes), so it is kept for A/B only
+// (XM_BQ_SPLIT=1); the product uses k_biquad_lanes.  Arithmetic per channel is
+// sosfilt's, unchanged.  Section 0 loads whole interleaved granules (both
+// channel lanes read the same 32 B) and keeps its channel; the last section
+// stores its channel's samples (the two channel lanes fill each 8-B frame).
+template <int CH, bool ST>
+__global__ __launch_bounds__(64) void k_biquad_split(XmhFxJob j)
+{
+    typedef const __attribute__((address_space(1))) bq_f4 gcf4;
+    constexpr int G = CH / 4;                      // mono granules (4 frames) per chunk
+    __shared__ bq_f4 in_buf[G][64];
+    __shared__ bq_f4 sec_buf[G][64];
+    const int ns = j.n_sos;
+    const int lpc = 2 * ns;                        // lanes per clip
+    const int kpw = 64 / lpc;
+    const int lane = threadIdx.x;
+    const int s = lane % ns, ch = (lane / ns) & 1, kk = lane / lpc;
+    const int clip = blockIdx.x * kpw + kk;
+    const bool valid = kk < kpw && clip < j.n_clips;
+    const bool first = s == 0, last = s == ns - 1;
+    const int64_t N = j.frames;
+    const int64_t nchunk = (N + CH - 1) / CH;
+    const float *x = valid ? j.in_ptrs[clip] : nullptr;
+    float *y = valid ? j.out_ptrs[clip] : nullptr;
+    const bq_f4 *src = first ? &in_buf[0][lane] : &sec_buf[0][(lane + 63) & 63];
+
+    const float *q = j.sos + 6 * s;
+    const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
+    float z0 = 0.0f, z1 = 0.0f;
+    float *st = (ST && valid) ? j.state + ((size_t)clip * ns + s) * 4 : nullptr;   // [z0 L,R][z1 L,R]
+    if (ST && st) { z0 = st[ch]; z1 = st[2 + ch]; }
+
+    bq_f4 pa[2 * G], pb[2 * G];                    // raw interleaved granules, chunks i and i + 1
+    auto load = [&](bq_f4 (&d)[2 * G], int64_t c) {
+        if (!(first && valid && c < nchunk)) return;
+        const float *xc = x + (size_t)2 * (size_t)(c * CH);
+        if ((c + 1) * CH <= N && (((uintptr_t)xc) & 15) == 0) {
+#pragma unroll
+            for (int g = 0; g < 2 * G; ++g) d[g] = ((gcf4 *)xc)[g];
+        } else {
+#pragma unroll
+            for (int g = 0; g < 2 * G; ++g)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    d[g][e] = (c * CH) * 2 + g * 4 + e < N * 2 ? xc[g * 4 + e] : 0.0f;
+        }
+    };
+    auto step = [&](int64_t i, bq_f4 (&cur)[2 * G]) {
+        if (first) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const bq_f4 u = cur[2 * g], w = cur[2 * g + 1];
+                in_buf[g][lane] = ch ? bq_f4{u[1], u[3], w[1], w[3]} : bq_f4{u[0], u[2], w[0], w[2]};
+            }
+        }
+        load(cur, i + 2);
+        const int64_t c = i - s;
+        bq_f4 v4[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) v4[g] = src[g * 64];
+        if (c >= 0 && c < nchunk) {
+            const bool tail = ST && st && (c + 1) * CH > N;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                bq_f4 r;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = v4[g][e];
+                    const float o = b0 * v + z0;          // sosfilt (_sosfilt.pyx) order
+                    if (!(tail && c * CH + g * 4 + e >= N)) {
+                        z0 = (b1 * v - a1 * o) + z1;
+                        z1 = b2 * v - a2 * o;
+                    }
+                    r[e] = o;
+                }
+                v4[g] = r;
+            }
+            if (!last) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) sec_buf[g][lane] = v4[g];
+            } else if (valid) {
+                float *yc = y + (size_t)2 * (size_t)(c * CH) + ch;
+                if ((c + 1) * CH <= N) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) yc[(g * 4 + e) * 2] = v4[g][e];
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (c * CH + g * 4 + e < N) yc[(g * 4 + e) * 2] = v4[g][e];
+                }
+            }
+        }
+    };
+    load(pa, 0);
+    load(pb, 1);
+    const int64_t steps = nchunk + ns - 1;
+    for (int64_t i = 0; i < steps; i += 2) {
+        step(i, pa);
+        if (i + 1 < steps) step(i + 1, pb);
+    }
+    if (ST && st) { st[ch] = z0; st[2 + ch] = z1; }
+}
+
 constexpr int FIR_THREADS = 256;
 constexpr int FIR_OPT = 4;
 constexpr int FIR_CHUNK = FIR_THREADS * FIR_OPT;
@@ -243,10 +357,21 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
 {
     if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
     if (j->n_clips == 0 || j->frames == 0) return 0;
-    const int kpw = 64 / j->n_sos;
+
+    // 64-frame chunks: half the per-chunk LDS hand-offs of 32 and one chunk
+    // more of compute to cover each prefetch (config 4: 24.06 -> 22.83 ms)
+    auto kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 64, true> : k_biquad_lanes<2, 64, true>)
+                         : (j->channels == 1 ? k_biquad_lanes<1, 64, false> : k_biquad_lanes<2, 64, false>);
+    if (const char *c = getenv("XM_BQ_CH"); c && atoi(c) == 32)   // A/B: the previous chunk length
+        kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 32, true> : k_biquad_lanes<2, 32, true>)
+                        : (j->channels == 1 ? k_biquad_lanes<1, 32, false> : k_biquad_lanes<2, 32, false>);
+    int lpc = j->n_sos;                                // lanes per clip
+    if (j->channels == 2 && getenv("XM_BQ_SPLIT")) {   // A/B only: one channel per lane (measured slower)
+        kern = j->state ? k_biquad_split<32, true> : k_biquad_split<32, false>;
+        lpc = 2 * j->n_sos;
+    }
+    const int kpw = 64 / lpc;
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    auto kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 32, true> : k_biquad_lanes<2, 32, true>)
-                         : (j->channels == 1 ? k_biquad_lanes<1, 32, false> : k_biquad_lanes<2, 32, false>);
     XmhFxJob jj = *j;
     if (const char *d = getenv("XM_FX_DEV")) jj.dev_flags = atoi(d);   // dev attribution knob
     hipLaunchKernelGGL(kern, grid, dim3(64), 0, (hipStream_t)stream, jj);
