@@ -10,10 +10,10 @@ import pytest
 from conftest import LIB_DIR, ROOT
 
 
-def _build(tmp_path):
-    exe = tmp_path / "xm_mix_example"
+def _build(tmp_path, name="xm_mix_example"):
+    exe = tmp_path / name
     cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "examples", "xm_mix_example.c"), "-L", LIB_DIR, "-lxm_audio",
+           os.path.join(ROOT, "examples", name + ".c"), "-L", LIB_DIR, "-lxm_audio",
            f"-Wl,-rpath,{LIB_DIR}", "-lm", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     return exe
@@ -40,3 +40,22 @@ def test_example_runs_on_gpu(tmp_path):
         assert "44100 frames" in ln
         rms = float(ln.rsplit("rms", 1)[1])
         assert 0.05 < rms < 2.0
+
+
+def test_stream_example_builds_and_refuses_without_gpu(tmp_path):
+    """The streaming / timeline entry points compile from plain C11 (-Werror)."""
+    exe = _build(tmp_path, "xm_stream_example")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    if "0 HIP device(s)" in p.stdout:
+        assert p.returncode == 2, p.stderr
+    else:
+        assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.gpu
+def test_stream_example_runs_on_gpu(tmp_path):
+    exe = _build(tmp_path, "xm_stream_example")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "bit-identical to process_batch" in p.stdout
+    assert "timeline: 44100 frames" in p.stdout
