@@ -30,6 +30,13 @@ extern "C" {
 typedef struct XmAudioMixer XmAudioMixer;
 struct XmEffects;
 
+/* XmMixerConfig.flags: write the output in the other sample format, converted
+ * in the kernels' store epilogue.  F32 mixers write
+ * s16 = saturate16(rint(y * 32768)) (ties to even); S16 mixers write
+ * f32 = y * 2^-15 (exact) of the saturated Q15 mix.  Output buffers and
+ * output strides are then in elements of the output format. */
+#define XM_MIXER_OUT_CONVERT 1u
+
 typedef struct XmMixerConfig {
     int32_t in_rate;      /* Hz, every track (per-track rates: XmTrackDesc.in_rate) */
     int32_t out_rate;     /* Hz of the mix */
@@ -37,7 +44,7 @@ typedef struct XmMixerConfig {
     int32_t sample_fmt;   /* XmSampleFmt, input and output */
     int32_t mem_kind;     /* XmMemKind of the in/out pointers */
     int32_t device;       /* HIP device ordinal the handle runs on */
-    int32_t flags;        /* reserved, 0 */
+    int32_t flags;        /* 0 or XM_MIXER_OUT_CONVERT */
     int32_t reserved;
 } XmMixerConfig;
 

@@ -100,10 +100,18 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
             int32_t *y = (int32_t *)xm_out_ptr(j, b, 4);
 #pragma unroll
             for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = acci[o][c];
+        } else if (S16 && j.out_conv == 2) {
+            float *y = (float *)xm_out_ptr(j, b, 4);
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = (float)xm_sat16(acci[o][c]) * 0x1p-15f;
         } else if (S16) {
             int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
 #pragma unroll
             for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = xm_sat16(acci[o][c]);
+        } else if (j.out_conv == 1) {
+            int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = (int16_t)xm_round_sat16(accf[o][c] * 32768.0f);
         } else {
             float *y = (float *)xm_out_ptr(j, b, 4);
 #pragma unroll
@@ -177,6 +185,12 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_s16(XmhMixJob j)
     int16_t o[SPT];
 #pragma unroll
     for (int i = 0; i < SPT; ++i) o[i] = xm_sat16(acc[i]);
+    if (j.out_conv == 2) {   // f32 output: exact scaling by 2^-15
+        float *yf = (float *)xm_out_ptr(j, b, 4) + s0;
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) yf[i] = (float)o[i] * 0x1p-15f;
+        return;
+    }
     int16_t *y = (int16_t *)xm_out_ptr(j, b, 2) + s0;
     if (full && ((((uintptr_t)y) & 15) == 0)) {
         int4 q;
@@ -220,6 +234,12 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_f32(XmhMixJob j)
 #pragma unroll
             for (int c = 0; c < C; ++c) acc[f * C + c] = acc[f * C + c] + gf * v[f * C + c];
         }
+    }
+    if (j.out_conv == 1) {   // s16 output: sat16(rint(y * 32768))
+        int16_t *yq = (int16_t *)xm_out_ptr(j, b, 2) + s0;
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) yq[i] = (int16_t)xm_round_sat16(acc[i] * 32768.0f);
+        return;
     }
     float *y = (float *)xm_out_ptr(j, b, 4) + s0;
     if (full && ((((uintptr_t)y) & 15) == 0)) {
@@ -278,10 +298,18 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_placed(XmhMixJob j)
             }
         }
     }
-    if (S16) {
+    if (S16 && j.out_conv == 2) {
+        float *y = (float *)xm_out_ptr(j, b, 4) + s0;
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) y[i] = (float)xm_sat16(acci[i]) * 0x1p-15f;
+    } else if (S16) {
         int16_t *y = (int16_t *)xm_out_ptr(j, b, 2) + s0;
         for (int i = 0; i < SPT; ++i)
             if (s0 + i < total) y[i] = xm_sat16(acci[i]);
+    } else if (j.out_conv == 1) {
+        int16_t *y = (int16_t *)xm_out_ptr(j, b, 2) + s0;
+        for (int i = 0; i < SPT; ++i)
+            if (s0 + i < total) y[i] = (int16_t)xm_round_sat16(accf[i] * 32768.0f);
     } else {
         float *y = (float *)xm_out_ptr(j, b, 4) + s0;
         for (int i = 0; i < SPT; ++i)
@@ -353,6 +381,7 @@ extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
     const bool s16 = j->fmt == 1;
     if (j->frames_out == 0 || j->n_mix == 0) return 0;
     if (j->partial && !s16) return -22;   // XM_EINVAL: partials are the s16 (Q15) mix
+    if (j->partial && j->out_conv) return -22;
     if (j->rs.L == j->rs.M) {
         const int spt = s16 ? 8 : 4;
         const int64_t samples = j->frames_out * C;

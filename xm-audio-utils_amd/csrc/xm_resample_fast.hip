@@ -744,7 +744,7 @@ extern "C" int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_laun
     const int NT = j->n_tracks;
     const int64_t N = j->frames_in;
     if (!(j->rs.L == L && j->rs.M == M && j->rs.rm == RM && j->rs.T == 23 && j->rs.fast) || j->in_base ||
-        j->out_base ||
+        j->out_base || j->out_conv ||
         j->fmt != 2 || j->channels != 2 || j->in_ptrs || j->out_ptrs || !j->gains_host ||
         N <= 0 || (N & 1) || N >= (1 << 26) || j->n_mix <= 0)
         return -1003;   // not this kernel's job: generic path

@@ -74,6 +74,10 @@ typedef struct XmhMixJob {
     /* timeline mix (xmh_launch_mix_placed): device [n_tracks][2] int64 =
      * (output frame of the track's first frame, track length in frames) */
     const int64_t *place;
+    /* output format conversion in the store epilogue (XM_MIXER_OUT_CONVERT):
+     * 0 none; 1 f32 mix -> s16 out = sat16(rint(y * 32768)); 2 s16 mix -> f32 out = y * 2^-15 */
+    int32_t out_conv;
+    int32_t reserved3;
 } XmhMixJob;
 
 /* ---------- effects job ---------------------------------------------------- */

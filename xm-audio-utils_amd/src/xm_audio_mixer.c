@@ -52,6 +52,13 @@ struct XmAudioMixer {
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
 
+/* output element size (XM_MIXER_OUT_CONVERT writes the other format) */
+static int out_bytes(const XmAudioMixer *m)
+{
+    const int conv = (m->cfg.flags & XM_MIXER_OUT_CONVERT) != 0;
+    return fmt_bytes(conv ? (m->cfg.sample_fmt == XM_FMT_S16 ? XM_FMT_F32 : XM_FMT_S16) : m->cfg.sample_fmt);
+}
+
 static int grow(void **p, size_t *cap, size_t need)
 {
     if (*cap >= need) return XM_OK;
@@ -71,7 +78,8 @@ XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status)
     XmAudioMixer *m = NULL;
     if (!cfg || cfg->in_rate <= 0 || cfg->out_rate <= 0 || (cfg->channels != 1 && cfg->channels != 2) ||
         (cfg->sample_fmt != XM_FMT_S16 && cfg->sample_fmt != XM_FMT_F32) ||
-        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) || cfg->device < 0) {
+        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) || cfg->device < 0 ||
+        (cfg->flags & ~(int32_t)XM_MIXER_OUT_CONVERT)) {
         rc = XM_EINVAL;
         goto out;
     }
@@ -239,6 +247,7 @@ static void job_init(XmAudioMixer *m, XmhMixJob *j, size_t batch, size_t frames_
     j->rs.rm = m->table.d.rm;
     j->rs.H = m->table.H_dev;
     j->rs.fast = m->table.fast;
+    if (m->cfg.flags & XM_MIXER_OUT_CONVERT) j->out_conv = m->cfg.sample_fmt == XM_FMT_F32 ? 1 : 2;
 }
 
 static int upload_gains(XmAudioMixer *m)
@@ -277,6 +286,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     if (rc) return rc;
     rc = xmh_memcpy_h2d(ug, &unity_gain, sizeof unity_gain, m->stream);
     XmhMixJob r = *j0;
+    r.out_conv = 0;   /* tracks stay f32 in scratch; the final mix converts */
     r.n_tracks = 1;
     r.n_mix = (int32_t)ntot;
     r.gains = ug;
@@ -431,7 +441,7 @@ static int process_device(XmAudioMixer *m, const void *const *in, void *const *o
     const void *const *din = NULL;
     void *const *dout = NULL;
     int in_strided = as_strided(in, batch, m->n_tracks, elem, &ts, &ms);
-    int out_strided = as_strided((const void *const *)out, batch, 1, elem, &dummy, &os);
+    int out_strided = as_strided((const void *const *)out, batch, 1, out_bytes(m), &dummy, &os);
     int rc = XM_OK;
     if (!in_strided || !out_strided)
         rc = ptr_table(m, in_strided ? NULL : in, in_strided ? 0 : batch * (size_t)m->n_tracks,
@@ -460,7 +470,7 @@ static int process_host(XmAudioMixer *m, const void *const *in, void *const *out
     const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->n_tracks;
     const size_t fout = xm_audio_mixer_out_frames(m, frames_in);
     const size_t in_track = frames_in * (size_t)C * (size_t)elem;
-    const size_t out_mix = fout * (size_t)C * (size_t)elem;
+    const size_t out_mix = fout * (size_t)C * (size_t)out_bytes(m);
     const size_t per_mix = in_track * (size_t)ntr + out_mix;
     size_t chunk = per_mix ? ((size_t)2 << 30) / per_mix : batch;   /* <= 2 GiB per chunk */
     if (chunk < 1) chunk = 1;
@@ -525,7 +535,8 @@ int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in, ptrdiff_
                                        size_t batch, size_t frames_in)
 {
     if (!m || (batch && (!in || !partial))) return XM_EINVAL;
-    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx || m->mixed_rates)
+    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx || m->mixed_rates ||
+        (m->cfg.flags & XM_MIXER_OUT_CONVERT))
         return XM_ENOSYS;
     if (batch == 0) return XM_OK;
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
@@ -585,7 +596,7 @@ int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in
         for (size_t b = 0; !rc && b < batch; ++b) {
             for (size_t tr = 0; tr < ntr; ++tr)
                 ip[b * ntr + tr] = (const char *)in + ((ptrdiff_t)b * in_mix_stride + (ptrdiff_t)tr * in_track_stride) * elem;
-            op[b] = (char *)out + (ptrdiff_t)b * out_mix_stride * elem;
+            op[b] = (char *)out + (ptrdiff_t)b * out_mix_stride * out_bytes(m);
         }
         if (!rc) rc = xm_audio_mixer_process_batch(m, (const void *const *)ip, (void *const *)op, batch, frames_in);
         free(ip);
@@ -663,6 +674,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     if (m->n_tracks != m->st_ntr) return XM_EINVAL;   /* track list changed mid-stream */
     const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->st_ntr;
     const size_t batch = m->st_batch, rows = batch * (size_t)ntr, fb = (size_t)C * (size_t)elem;
+    const size_t ofb = (size_t)C * (size_t)out_bytes(m);   /* output frame bytes */
     const int64_t R = m->st_recv + (int64_t)n;
     int64_t mend = st_ready_out(m, R, flush);
     if (mend < m->st_out) mend = m->st_out;
@@ -710,7 +722,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     /* 2) the outputs that are now final */
     if (nout) {
         int host = m->cfg.mem_kind != XM_MEM_DEVICE;
-        if (host && (rc = grow(&m->d_out, &m->d_out_cap, batch * nout * fb + 16))) return rc;
+        if (host && (rc = grow(&m->d_out, &m->d_out_cap, batch * nout * ofb + 16))) return rc;
         XmhMixJob j;
         job_init(m, &j, batch, (size_t)R);
         j.frames_out = (int64_t)nout;
@@ -724,7 +736,8 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
         j.out_mix_stride = host ? (int64_t)(nout * (size_t)C) : (int64_t)os;
         rc = run_job(m, &j);
         if (!rc && host)
-            rc = xmh_memcpy2d(out, (size_t)os * (size_t)elem, m->d_out, nout * fb, nout * fb, batch, m->stream);
+            rc = xmh_memcpy2d(out, (size_t)os * (size_t)out_bytes(m), m->d_out, nout * ofb, nout * ofb, batch,
+                              m->stream);
         if (rc) return rc;
     }
     if (m->cfg.mem_kind != XM_MEM_DEVICE) {   /* host buffers are the caller's again on return */
@@ -845,6 +858,7 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
         j.out_ptrs = dout;
         j.gains = m->gains_dev;
         j.place = m->place_dev;
+        if (m->cfg.flags & XM_MIXER_OUT_CONVERT) j.out_conv = m->cfg.sample_fmt == XM_FMT_F32 ? 1 : 2;
         rc = xmh_launch_mix_placed(&j, m->stream, &launches);
     }
     if (!rc) rc = xmh_event_record(m->ev[3], m->stream);
@@ -878,9 +892,9 @@ int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, cons
         toff[tr] = in_bytes;
         in_bytes += (size_t)place[tr].frames_in * (size_t)C * (size_t)elem + 256;
     }
-    const size_t out_bytes = out_frames * (size_t)C * (size_t)elem;
+    const size_t out_mix_bytes = out_frames * (size_t)C * (size_t)out_bytes(m);
     rc = grow(&m->d_in, &m->d_in_cap, in_bytes + 16);
-    if (!rc) rc = grow(&m->d_out, &m->d_out_cap, out_bytes + 16);
+    if (!rc) rc = grow(&m->d_out, &m->d_out_cap, out_mix_bytes + 16);
     const void *dp[XM_MAX_TRACKS];
     void *dop[1];
     for (size_t b = 0; !rc && b < batch; ++b) {
@@ -891,7 +905,7 @@ int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, cons
         }
         dop[0] = m->d_out;
         if (!rc) rc = timeline_device(m, dp, place, dop, 1, out_frames);
-        if (!rc) rc = xmh_memcpy_d2h(out[b], m->d_out, out_bytes, m->stream);
+        if (!rc) rc = xmh_memcpy_d2h(out[b], m->d_out, out_mix_bytes, m->stream);
         if (!rc) rc = xmh_stream_sync(m->stream);
     }
     return finish(m, rc);

@@ -38,6 +38,7 @@ _lib = C.CDLL(LIB_PATH)
 XM_OK, XM_EINVAL, XM_ENOMEM, XM_EDEVICE, XM_ECOMM, XM_ENOSYS = 0, -22, -12, -1001, -1002, -1003
 XM_FMT_S16, XM_FMT_F32 = 1, 2
 XM_MEM_HOST, XM_MEM_DEVICE = 0, 1
+XM_MIXER_OUT_CONVERT = 1
 XM_GAIN_RAMP, XM_GAIN_XFADE_OUT = 0, 1
 XM_EQ_PEAKING, XM_EQ_LOWSHELF, XM_EQ_HIGHSHELF, XM_EQ_LOWPASS, XM_EQ_HIGHPASS = range(5)
 FMT = {"s16": XM_FMT_S16, "f32": XM_FMT_F32}
@@ -208,8 +209,9 @@ class Mixer:
     """xm_audio_mixer_* handle."""
 
     def __init__(self, in_rate: int, out_rate: int, channels: int = 2, fmt: str = "f32",
-                 mem: str = "host", device: int = 0):
-        cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device, 0, 0)
+                 mem: str = "host", device: int = 0, convert_out: bool = False):
+        cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device,
+                            XM_MIXER_OUT_CONVERT if convert_out else 0, 0)
         st = C.c_int(0)
         self._h = _lib.xm_audio_mixer_create_ex(C.byref(cfg), C.byref(st))
         if not self._h:
@@ -217,6 +219,7 @@ class Mixer:
         self.cfg = cfg
         self.fmt = FMT[fmt]
         self.dtype = DTYPE[self.fmt]
+        self.out_dtype = (np.float32 if self.fmt == XM_FMT_S16 else np.int16) if convert_out else self.dtype
         self.channels = channels
         self.n_tracks = 1
 
@@ -257,7 +260,7 @@ class Mixer:
         x = np.ascontiguousarray(x, self.dtype)
         assert x.ndim == 4 and x.shape[1] == self.n_tracks and x.shape[3] == self.channels, x.shape
         B, ntr, N, Cc = x.shape
-        y = np.empty((B, self.out_frames(N), Cc), self.dtype)
+        y = np.empty((B, self.out_frames(N), Cc), self.out_dtype)
         base, ts = x.ctypes.data, N * Cc * x.itemsize
         ins = (C.c_void_p * (B * ntr))(*[base + i * ts for i in range(B * ntr)])
         ob, os_ = y.ctypes.data, y.shape[1] * Cc * y.itemsize
@@ -276,7 +279,7 @@ class Mixer:
         ts = [np.ascontiguousarray(t, self.dtype) for t in tracks]
         assert len(ts) == self.n_tracks == len(offsets)
         B = ts[0].shape[0]
-        y = np.empty((B, out_frames, self.channels), self.dtype)
+        y = np.empty((B, out_frames, self.channels), self.out_dtype)
         ins = (C.c_void_p * (B * len(ts)))(*[t[b].ctypes.data if t.shape[1] else y.ctypes.data
                                              for b in range(B) for t in ts])
         pl = (XmTrackPlacement * len(ts))(*[XmTrackPlacement(int(o), t.shape[1]) for o, t in zip(offsets, ts)])
@@ -299,7 +302,7 @@ class Mixer:
         B, ntr, N, Cc = x.shape
         assert B == self._st_batch and ntr == self.n_tracks and Cc == self.channels, x.shape
         n = self.stream_out_frames(N)
-        y = np.empty((B, max(n, 1), Cc), self.dtype)
+        y = np.empty((B, max(n, 1), Cc), self.out_dtype)
         got = C.c_size_t(0)
         _check(_lib.xm_audio_mixer_stream_push(self._h, x.ctypes.data if x.size else None, N * Cc, ntr * N * Cc,
                                                N, y.ctypes.data, y.shape[1] * Cc, y.shape[1], C.byref(got)),
@@ -323,7 +326,7 @@ class Mixer:
 
     def stream_flush(self) -> np.ndarray:
         n = self.stream_out_frames(0, True)
-        y = np.empty((self._st_batch, max(n, 1), self.channels), self.dtype)
+        y = np.empty((self._st_batch, max(n, 1), self.channels), self.out_dtype)
         got = C.c_size_t(0)
         _check(_lib.xm_audio_mixer_stream_flush(self._h, y.ctypes.data, y.shape[1] * self.channels, y.shape[1],
                                                 C.byref(got)), "stream_flush")
