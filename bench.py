@@ -2,9 +2,11 @@
 """Headline benchmark: PCM Msamples/s for 48 kHz -> 44.1 kHz polyphase
 resample + 8-track gain-ramped mixdown (BASELINE.json:2).
 
-Workload per GPU (weak scaling): 4096 input clips =
-512 mixes x 8 tracks, 10 s stereo fp32 @ 48 kHz (480000 frames) ->
-512 mixes x 441000 frames stereo fp32 @ 44.1 kHz.  Inputs are synthetic
+Workload (strong scaling, SURVEY.md §8(d) "keep it fixed across 1/2/4/8
+GPUs"): 4096 input clips in total = 512 mixes x 8 tracks, 10 s
+stereo fp32 @ 48 kHz (480000 frames) -> 512 mixes x 441000 frames stereo
+fp32 @ 44.1 kHz, split into N contiguous blocks of 512/N mixes, one per GPU.
+`--weak` instead keeps 512 mixes on every GPU (labelled "weak").  Inputs are synthetic
 (splitmix64 PCM) generated directly in HBM by the
 library's xm_synth_pcm, outside the timed region.  One step = one
 xm_audio_mixer_process_strided call over the whole per-GPU batch (every
@@ -23,7 +25,9 @@ Also reported (one JSON line on rank 0):
                  the stream the kernel runs on, vs the 8 TB/s HBM peak;
                  traffic from the rocprofv3 PMC pass in profiles/ if present.
   cpu_baseline — the C restatement (oracle/, "port") on a bounded sample of
-                 the same workload on this host's cores.
+                 the same workload on this host's cores, and on 1 core.
+  parity_check — after the timed loop every rank bit-compares the first and
+                 the last mix of its block with the oracle (true = all equal).
 """
 from __future__ import annotations
 
@@ -64,7 +68,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mixes", type=int, default=512, help="mixes per GPU (x8 tracks = clips)")
+    ap.add_argument("--global-clips", type=int, default=4096,
+                    help="input clips over all GPUs (strong scaling; 8 tracks per mix)")
+    ap.add_argument("--weak", action="store_true", help="keep --mixes mixes on every GPU instead")
+    ap.add_argument("--mixes", type=int, default=512, help="mixes per GPU with --weak")
     ap.add_argument("--tracks", type=int, default=8)
     ap.add_argument("--frames", type=int, default=480000, help="input frames per track (10 s @ 48 kHz)")
     ap.add_argument("--cpu-mixes", type=int, default=48, help="mixes in the CPU-baseline sample")
@@ -72,7 +79,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fill", choices=["synth", "zero", "tiny"], default="synth",
                     help="dev only: input data (synth = the bench's synthetic PCM)")
-    ap.add_argument("--check", action="store_true", help="bit-compare 2 mixes with the oracle after timing")
+    ap.add_argument("--no-check", action="store_true", help="skip the post-timing parity check")
+    ap.add_argument("--check", action="store_true", help=argparse.SUPPRESS)   # the default now
     return ap.parse_args()
 
 
@@ -89,9 +97,22 @@ def traffic_from_profiles():
         return None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, ramps):
+    """The oracle's C restatement (same arithmetic) on a bounded sample of the
+    workload: whole passes over --cpu-mixes mixes on every allotted core for
+    about --cpu-seconds, then on one core for about a quarter of that."""
     import c_oracle as CO
-    import np_oracle as O
     nmix = args.cpu_mixes
     x = np.empty((nmix, args.tracks, args.frames, 2), np.float32)
     for b in range(nmix):
@@ -99,19 +120,35 @@ def cpu_baseline(args, ramps):
             x[b, t] = CO.gen_f32(SEED, b * args.tracks + t, 2, args.frames)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
-    # whole passes over the same bounded sample until about --cpu-seconds of wall time
-    passes, dt = 0, 0.0
-    while passes == 0 or (dt < args.cpu_seconds and passes < 200):
-        t0 = time.perf_counter()
-        _, used = CO.batch_resample_mix_f32(x, ramps, 147, 160, threads=threads)
-        dt += time.perf_counter() - t0
-        passes += 1
-    samples = x.size * passes
+
+    def run(xs, nth, seconds):
+        passes, dt, used = 0, 0.0, 1
+        while passes == 0 or (dt < seconds and passes < 200):
+            t0 = time.perf_counter()
+            _, used = CO.batch_resample_mix_f32(xs, ramps, 147, 160, threads=nth)
+            dt += time.perf_counter() - t0
+            passes += 1
+        return xs.size * passes, dt, passes, used
+
+    samples, dt, passes, used = run(x, threads, args.cpu_seconds)
+    x1 = x[:2]
+    s1, dt1, p1, _ = run(x1, 1, args.cpu_seconds / 4)
     del x
     return {"value": round(samples / dt / 1e6, 2), "unit": "Msamples/s", "cores": int(used), "kind": "port",
+            "value_1core": round(s1 / dt1 / 1e6, 2), "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{passes} passes over {nmix} mixes x {args.tracks} tracks x {args.frames} frames x 2 ch fp32 "
-                      f"({samples / 1e6:.0f} M input samples, {dt:.2f} s wall, {threads} threads), "
-                      f"oracle/xm_oracle.c -O3 -ffp-contract=off, OpenMP over mixes"}
+                      f"({samples / 1e6:.0f} M input samples, {dt:.2f} s wall, {used} threads); 1 core: {p1} passes "
+                      f"over 2 mixes ({s1 / 1e6:.0f} M samples, {dt1:.2f} s); oracle/xm_oracle.c -O3 "
+                      f"-ffp-contract=off, OpenMP over mixes"}
+
+
+def parity_check(x, y, idx, ramps):
+    """Bit-compare mixes `idx` of this rank's output with the oracle."""
+    import c_oracle as CO
+    xs = x[list(idx)].cpu().numpy()
+    ref, _ = CO.batch_resample_mix_f32(xs, ramps, 147, 160, threads=min(len(idx), os.cpu_count() or 1))
+    got = y[list(idx)].cpu().numpy()
+    return bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
 
 
 def main():
@@ -125,7 +162,13 @@ def main():
     xd.init(rk, "nccl", torch.device("cuda", rk.local))   # RCCL; barrier + max-time only
     dev = torch.cuda.current_device()
 
-    B, ntr, N = args.mixes, args.tracks, args.frames
+    ntr, N = args.tracks, args.frames
+    if args.weak:
+        B = args.mixes
+    else:
+        if args.global_clips % (ntr * world):
+            raise SystemExit(f"--global-clips {args.global_clips} does not split into whole mixes over {world} GPUs")
+        B = args.global_clips // (ntr * world)
     ramps = RAMPS[:ntr] if ntr <= len(RAMPS) else (RAMPS * ((ntr + 7) // 8))[:ntr]
     mixer = xm.Mixer(48000, 44100, 2, "f32", mem="device", device=dev)
     mixer.set_tracks(ramps)
@@ -166,11 +209,9 @@ def main():
     elapsed = xd.max_over_ranks(rk, elapsed, device="cuda")
 
     ok = None
-    if args.check and rank == 0:
-        import c_oracle as CO
-        xs = x[:2].cpu().numpy()
-        ref, _ = CO.batch_resample_mix_f32(xs, ramps, 147, 160, threads=os.cpu_count() or 1)
-        ok = bool(np.array_equal(y[:2].cpu().numpy().view(np.uint32), ref.view(np.uint32)))
+    if not args.no_check:   # every rank: its first and last mix vs the oracle
+        ok = parity_check(x, y, sorted({0, B - 1}), ramps)
+        ok = xd.min_over_ranks(rk, ok, device="cuda")
 
     in_samples = B * ntr * N * 2
     ms_per_step = elapsed / args.steps * 1e3
@@ -186,11 +227,12 @@ def main():
             "metric": "PCM Msamples/sec (48k->44.1k resample + 8-track mix), batch 4096, 1/2/4/8 GPUs",
             "value": round(value, 1), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "48k->44.1k polyphase resample (scipy resample_poly order) + 8-track "
                                    "gain-ramp/crossfade mixdown, stereo fp32, 10 s clips",
                        "clips_per_gpu": B * ntr, "mixes_per_gpu": B, "tracks": ntr, "frames_in": N,
                        "frames_out": F, "channels": 2, "global_clips": world * B * ntr,
+                       "global_mixes": world * B,
                        "parallelism": f"dp{world} (independent mixes, no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -200,7 +242,8 @@ def main():
             "cpu_baseline": cpu,
         }
         if ok is not None:
-            line["parity_check_2mixes"] = ok
+            line["parity_check"] = ok
+            line["parity_detail"] = "bit-exact vs oracle/xm_oracle.c: first and last mix of every rank's block"
         print(json.dumps(line), flush=True)
     xd.finish(rk)
 

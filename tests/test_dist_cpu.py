@@ -82,20 +82,58 @@ def test_two_rank_shards_union_equals_single_process():
 
 
 # ---- config 5 (BASELINE.json:11): tracks of every mix spread over the ranks
-B5, NT5, F5 = 4, 16, 3001
-RAMPS5 = [dict(gain0_q15=q, gain1_q15=q2, ramp_start=s, ramp_len=ln, mode=md)
-          for q, q2, s, ln, md in [(32768, 32768, 0, 0, 0), (0, 32768, 100, 2000, 0), (65535, 100, 0, 3001, 0),
-                                   (16384, 16384, 0, 0, 0), (0, 0, 500, 900, 1), (0, 32768, 500, 900, 0),
-                                   (40000, 3, 2000, 13, 0), (7, 60000, 1500, 0, 0)] * 2]
+B5, NT5, F5 = 4, 64, 3001
+_R5 = [(32768, 32768, 0, 0, 0), (0, 32768, 100, 2000, 0), (65535, 100, 0, 3001, 0),
+       (16384, 16384, 0, 0, 0), (0, 0, 500, 900, 1), (0, 32768, 500, 900, 0),
+       (40000, 3, 2000, 13, 0), (7, 60000, 1500, 0, 0)]
+RAMPS5 = [dict(gain0_q15=q, gain1_q15=q2, ramp_start=s, ramp_len=ln, mode=md) for q, q2, s, ln, md in _R5 * 8]
 
 
 def _tracks5(b):
     import np_oracle as O
     from bench import SEED
     tr = [O.gen_s16(SEED, 64 * b + t, 2, F5) for t in range(NT5)]
-    for t in range(4):              # loud tracks: the 16-track sum saturates
+    for t in range(6):              # loud tracks: the 64-track sum saturates
         tr[t][50:150] = 32767
+        tr[NT5 - 1 - t][400:480] = -32768
     return tr
+
+
+class _OracleMixer:
+    """CPU stand-in for the two config-5 entry points of xmaudio.Mixer
+    (process_partial_strided / finish_s16: same pointer-and-stride
+    signatures, host memory), so the gloo test drives xmaudio.dist's own
+    mix_spanning_s16 end to end.  The kernels themselves are GPU-tested."""
+
+    def __init__(self, ramps):
+        self.ramps = ramps
+
+    def out_frames(self, n):
+        return n                    # 48 kHz -> 48 kHz
+
+    @staticmethod
+    def _view(ptr, dtype, n):
+        import ctypes
+        return np.ctypeslib.as_array((ctypes.c_byte * (n * np.dtype(dtype).itemsize)).from_address(ptr)).view(dtype)
+
+    def process_partial_strided(self, in_ptr, ts, ms, part_ptr, pms, batch, frames):
+        import np_oracle as O
+        C = 2
+        x = self._view(in_ptr, np.int16, batch * ms)
+        part = self._view(part_ptr, np.int32, batch * pms)
+        for b in range(batch):
+            tracks = [x[b * ms + t * ts: b * ms + t * ts + frames * C].reshape(frames, C)
+                      for t in range(len(self.ramps))]
+            part[b * pms: b * pms + frames * C] = O.mix_s16_partial(tracks, self.ramps).reshape(-1)
+
+    def finish_s16(self, parts_ptr, n_parts, part_stride, pms, out_ptr, oms, batch, out_frames):
+        import np_oracle as O
+        assert n_parts == 1
+        S = out_frames * 2
+        p = self._view(parts_ptr, np.int32, batch * pms)
+        o = self._view(out_ptr, np.int16, batch * oms)
+        for b in range(batch):
+            o[b * oms: b * oms + S] = O.sat16(p[b * pms: b * pms + S].astype(np.int64))
 
 
 def _worker5(rank, world, port, q):
@@ -104,27 +142,25 @@ def _worker5(rank, world, port, q):
     for p in (os.path.join(ROOT, "xm-audio-utils_amd"), os.path.join(ROOT, "oracle"), ROOT):
         sys.path.insert(0, p)
     import torch
-    import np_oracle as O
     from xmaudio import dist as xd
 
     rk = xd.from_env()
     xd.init(rk, "gloo")
     per = NT5 // world
     mine = range(per * rank, per * (rank + 1))        # this rank's tracks of every mix
-    part = np.stack([O.mix_s16_partial([_tracks5(b)[t] for t in mine], [RAMPS5[t] for t in mine]).reshape(-1)
-                     for b in range(B5)])
-    blk = xd.reduce_partials(rk, torch.from_numpy(part))
+    x = torch.from_numpy(np.stack([np.stack([_tracks5(b)[t] for t in mine]) for b in range(B5)]))
+    y = xd.mix_spanning_s16(rk, _OracleMixer([RAMPS5[t] for t in mine]), x)
     first, n = xd.owned_mixes(rk, B5)
-    y = O.sat16(blk.numpy().astype(np.int64)).reshape(n, F5, 2)
+    assert y.shape == (n, F5, 2)
     xd.finish(rk)
-    q.put((rank, first, y))
+    q.put((rank, first, y.numpy()))
 
 
 def test_two_rank_spanning_mixdown_equals_full_mix():
-    """Config 5 exchange on CPU: each rank holds half of the 16 tracks of every
-    mix, forms the int32 Q15 partial, the partials meet in reduce_partials
-    (RCCL reduce-scatter on GPUs; all-reduce + block on gloo) and the owner
-    saturates: every mix equals the one-process 16-track mix bit for bit."""
+    """Config 5 exchange on CPU: each rank holds half of the 64 tracks of every
+    mix, forms the int32 Q15 partial, the partials meet in reduce_partials (one
+    reduce-scatter, RCCL on GPUs and gloo here) and the owner saturates: every
+    mix equals the one-process 64-track mix bit for bit, saturation included."""
     import np_oracle as O
     world = 2
     ctx = mp.get_context("spawn")
@@ -142,6 +178,9 @@ def test_two_rank_spanning_mixdown_equals_full_mix():
         for i in range(y.shape[0]):
             got[first + i] = y[i]
     assert sorted(got) == list(range(B5))
+    sat = 0
     for b in range(B5):
         want = O.mix_s16(_tracks5(b), RAMPS5)
+        sat += int(np.sum(np.abs(want.astype(np.int32)) >= 32767))
         assert np.array_equal(got[b], want), b
+    assert sat > 0                  # the test exercises saturation

@@ -175,20 +175,45 @@ def test_effects_stream_errors(xm, gpu):
         e.process_stream(x)
 
 
-@pytest.mark.parametrize("knob", [("XM_BQ_CH", "32"), ("XM_BQ_SPLIT", "1")])
-def test_biquad_ab_variants_stay_exact(xm, gpu, monkeypatch, knob):
-    """The A/B kernel variants (32-frame chunks; one channel per lane) keep the
-    bits, whole-clip and streamed, so a later switch of default is safe."""
-    z = golden("effects.npz")
-    x = np.stack([O.gen_f32(SEED, 3500 + b, 2, 5000 + 3) for b in range(7)])
-    monkeypatch.setenv(*knob)
-    e = xm.Effects(48000, 2)
-    for s in z["sos"]:
-        e.add_biquad(s)
-    y = e.process(x)
-    e.stream_reset(7)
-    ys = np.concatenate([e.process_stream(x[:, :1001]), e.process_stream(x[:, 1001:1002]),
-                         e.process_stream(x[:, 1002:])], axis=1)
-    for b in range(7):
-        r = CO.biquad_f32(x[b], z["sos"])
-        assert bits_equal(y[b], r) and bits_equal(ys[b], r), b
+def test_stream_device_1frame_reused_buffer(xm, gpu):
+    """Device-memory pushes that release no output (1-frame blocks) are still
+    synchronous on the handle's own stream: the caller refills ONE input
+    buffer between pushes from another stream, and the stream must have read
+    every block before the push returned (the nout == 0 path)."""
+    import torch
+    B, ntr, N = 2, 8, 700
+    x = np.stack([np.stack([O.gen_f32(SEED, 4100 + 8 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks(RAMPS8)
+    h = xm.Mixer(48000, 44100, 2, "f32")
+    h.set_tracks(RAMPS8)
+    want = h.process(x)
+    F = h.out_frames(N)
+    blk = torch.empty((B, ntr, 1, 2), dtype=torch.float32, device="cuda")
+    out = torch.zeros((B, F, 2), dtype=torch.float32, device="cuda")
+    side = torch.cuda.Stream()
+    m.stream_begin(B)
+    pos = 0
+    for f in range(N):
+        with torch.cuda.stream(side):     # refill the one buffer from another stream
+            blk.copy_(torch.from_numpy(x[:, :, f:f + 1]).pin_memory().cuda(non_blocking=True), non_blocking=True)
+        side.synchronize()
+        o = out[:, pos:]
+        pos += m.stream_push_strided(blk.data_ptr(), 2, ntr * 2, 1, o.data_ptr(), F * 2, F - pos)
+    o = out[:, pos:]
+    pos += m.stream_flush_strided(o.data_ptr(), F * 2, F - pos)
+    assert pos == F
+    assert bits_equal(out.cpu().numpy(), want)
+
+
+def test_stream_mixed_rates_mid_stream(xm, gpu):
+    """set_tracks with a per-track rate after stream_begin (same track count):
+    the next push refuses (XM_ENOSYS) instead of ignoring the rate."""
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(RAMPS8[:2])
+    m.stream_begin(1)
+    m.stream_push(np.zeros((1, 2, 100, 2), np.float32))
+    m.set_tracks([dict(RAMPS8[0]), dict(RAMPS8[1], in_rate=44100)])
+    with pytest.raises(xm.XmError) as e:
+        m.stream_push(np.zeros((1, 2, 100, 2), np.float32))
+    assert e.value.code == xm.XM_ENOSYS

@@ -109,3 +109,19 @@ def test_timeline_device_memory(xm, gpu):
     outs = (ctypes.c_void_p * 1)(yd.data_ptr())
     assert xm._lib.xm_audio_mixer_process_timeline(dev._h, ins, pl, outs, 1, 5000) == 0
     assert bits_equal(yd.cpu().numpy(), want[0])
+
+
+def test_rate_table_cache_follows_track_list(xm, gpu):
+    """Per-track rate tables are kept only while a track uses them: a handle
+    that sees more than 64 distinct rates over its life keeps working, and
+    the mix after many swaps equals a fresh handle's."""
+    m = xm.Mixer(44100, 48000, 1, "f32")
+    for r in range(8000, 8000 + 70 * 100, 100):        # 140 distinct rates, two at a time
+        m.set_tracks([dict(in_rate=r), dict(in_rate=r + 50, gain0=0.5)])
+    x = [np.stack([O.gen_f32(SEED, 7700 + b, 1, 3000)]) for b in range(2)]
+    tracks = [dict(in_rate=22050, gain0=0.7), dict(in_rate=16000, gain0=0.4)]
+    m.set_tracks(tracks)
+    y = m.process_timeline(x, [0, 100], 7000)
+    f = xm.Mixer(44100, 48000, 1, "f32")
+    f.set_tracks(tracks)
+    assert bits_equal(y, f.process_timeline(x, [0, 100], 7000))

@@ -14,7 +14,8 @@ done
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="--steps 10 --warmup 2 --no-cpu"
+DRIVER="--gpus 1 --steps 20 --warmup 5"          # the driver's bench command line
+PMCB="--steps 3 --warmup 1 --no-cpu --no-check"
 step() {   # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   echo "== $name: $*"
@@ -29,10 +30,13 @@ if [ $TESTS = 1 ]; then
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
-step bench 400 python3 -u bench.py --check
+step bench 400 python3 -u bench.py $DRIVER
 if [ $PROF = 1 ]; then
-  step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $BENCH
-  step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu
-  step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+  # the same invocation under the kernel-trace profiler: its bench line and
+  # its per-kernel average come from one run (profiles/<tag>_trace_bench.json)
+  step trace 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $DRIVER
+  step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py $PMCB
+  step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py $PMCB
+  step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES -d $OUT/pmc_sq -o run --output-format csv -- python3 bench.py $PMCB
 fi
 echo "gpu_check done: $OUT"

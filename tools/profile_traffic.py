@@ -64,6 +64,63 @@ def main():
     with open(dst + "_traffic.json", "w") as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec, indent=1))
+    trace_bench(src, dst)
+    sq_counters(src, dst)
+
+
+def trace_bench(src, dst):
+    """The bench line printed by the profiled run itself (trace.log) next to
+    the per-dispatch kernel durations of that same run: the timed launches are
+    the last `steps` dispatches of the headline kernel."""
+    line = None
+    log = os.path.join(src, "trace.log")
+    if os.path.exists(log):
+        for ln in open(log):
+            if ln.startswith("{"):
+                line = json.loads(ln)
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if line is None or not os.path.exists(tr):
+        return
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr))
+            if KERNEL in r["Kernel_Name"]]
+    timed = durs[-line["steps"]:]
+    avg_ms = sum(timed) / len(timed) / 1e6
+    alg = line["roofline"]["alg_bytes_per_launch"]
+    rec = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps 20 --warmup 5",
+           "bench_line": line,
+           "rocprof_timed_launches": len(timed),
+           "rocprof_avg_launch_ms": avg_ms,
+           "rocprof_frac": alg / (avg_ms * 1e-3) / 8.0e12,
+           "event_avg_launch_ms": line["roofline"]["avg_launch_ms"],
+           "event_frac": line["roofline"]["frac"],
+           "rocprof_over_event": avg_ms / line["roofline"]["avg_launch_ms"]}
+    with open(dst + "_trace_bench.json", "w") as fh:
+        json.dump(rec, fh, indent=1)
+    print(json.dumps({k: v for k, v in rec.items() if k != "bench_line"}, indent=1))
+
+
+def sq_counters(src, dst):
+    """SQ instruction counts per launch of the headline kernel (pmc_sq pass)
+    against the tap minimum: 512 mixes x 8 tracks x 441000 outputs x 44
+    packed VALU per output pair's half (22 taps x (mul + add) per channel
+    pair) / 64 lanes."""
+    f = os.path.join(src, "pmc_sq", "run_counter_collection.csv")
+    if not os.path.exists(f):
+        return
+    per = {}
+    for r in csv.DictReader(open(f)):
+        if KERNEL not in r["Kernel_Name"]:
+            continue
+        per.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
+        per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    rec = {c: sum(v.values()) / len(v) for c, v in per.items()}
+    tap_min = 512 * 8 * 441000 * 44 / 64
+    rec["valu_tap_minimum"] = tap_min
+    if "SQ_INSTS_VALU" in rec:
+        rec["valu_over_tap_minimum"] = rec["SQ_INSTS_VALU"] / tap_min
+    with open(dst + "_sq.json", "w") as fh:
+        json.dump(rec, fh, indent=1)
+    print(json.dumps(rec, indent=1))
 
 
 if __name__ == "__main__":

@@ -138,9 +138,15 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
     load(pa, 0);
     load(pb, 1);
     const int64_t steps = nchunk + ns - 1;
+    // Lane s reads, at step i, what lane s - 1 wrote at step i - 1: a
+    // cross-lane hand-off through LDS.  The wave barrier between steps orders
+    // every LDS access of step i before every one of step i + 1 for the
+    // compiler as well (free in a one-wave workgroup).
     for (int64_t i = 0; i < steps; i += 2) {
         step(i, pa);
+        __builtin_amdgcn_wave_barrier();
         if (i + 1 < steps) step(i + 1, pb);
+        __builtin_amdgcn_wave_barrier();
     }
     if (ST && st) {
         if constexpr (C == 2) { st[0] = z0.x; st[1] = z0.y; st[2] = z1.x; st[3] = z1.y; }
@@ -255,9 +261,11 @@ __global__ __launch_bounds__(64) void k_biquad_split(XmhFxJob j)
     load(pa, 0);
     load(pb, 1);
     const int64_t steps = nchunk + ns - 1;
-    for (int64_t i = 0; i < steps; i += 2) {
+    for (int64_t i = 0; i < steps; i += 2) {   // cross-lane LDS hand-off: see k_biquad_lanes
         step(i, pa);
+        __builtin_amdgcn_wave_barrier();
         if (i + 1 < steps) step(i + 1, pb);
+        __builtin_amdgcn_wave_barrier();
     }
     if (ST && st) { st[ch] = z0; st[2 + ch] = z1; }
 }
@@ -362,18 +370,24 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
     // more of compute to cover each prefetch (config 4: 24.06 -> 22.83 ms)
     auto kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 64, true> : k_biquad_lanes<2, 64, true>)
                          : (j->channels == 1 ? k_biquad_lanes<1, 64, false> : k_biquad_lanes<2, 64, false>);
-    if (const char *c = getenv("XM_BQ_CH"); c && atoi(c) == 32)   // A/B: the previous chunk length
+    int lpc = j->n_sos;                                // lanes per clip
+    XmhFxJob jj = *j;
+    jj.dev_flags = 0;
+#ifdef XM_FX_DEVKNOBS
+    // dev builds only (`make ablate`): A/B and attribution knobs.  XM_FX_DEV=1
+    // skips section 0's loads (wrong results by design), so the shipped
+    // library never reads these variables.
+    if (const char *c = getenv("XM_BQ_CH"); c && atoi(c) == 32)   // the previous chunk length
         kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 32, true> : k_biquad_lanes<2, 32, true>)
                         : (j->channels == 1 ? k_biquad_lanes<1, 32, false> : k_biquad_lanes<2, 32, false>);
-    int lpc = j->n_sos;                                // lanes per clip
-    if (j->channels == 2 && getenv("XM_BQ_SPLIT")) {   // A/B only: one channel per lane (measured slower)
+    if (j->channels == 2 && getenv("XM_BQ_SPLIT")) {   // one channel per lane (measured slower)
         kern = j->state ? k_biquad_split<32, true> : k_biquad_split<32, false>;
         lpc = 2 * j->n_sos;
     }
+    if (const char *d = getenv("XM_FX_DEV")) jj.dev_flags = atoi(d);
+#endif
     const int kpw = 64 / lpc;
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    XmhFxJob jj = *j;
-    if (const char *d = getenv("XM_FX_DEV")) jj.dev_flags = atoi(d);   // dev attribution knob
     hipLaunchKernelGGL(kern, grid, dim3(64), 0, (hipStream_t)stream, jj);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }

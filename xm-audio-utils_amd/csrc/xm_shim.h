@@ -128,8 +128,10 @@ int  xmh_pointer_is_device(const void *p);     /* 1 device, 0 host, <0 error */
 const char *xmh_arch_name(void);
 
 /* ---------- kernels ----------------------------------------------------------- */
-/* resample (if rs.L != rs.M) + gain + ordered track sum; returns launches made */
-int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches);
+/* resample (if rs.L != rs.M) + gain + ordered track sum; adds the launches
+ * made to *n_launches and, if the fused 147/160 kernel took the job, 1 to
+ * *n_fast (either pointer may be NULL) */
+int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches, int *n_fast);
 int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
 /* timeline mix: out[m] = ordered sum over tracks of g_tr(m) * x_tr[m - place_tr.offset],
  * x_tr zero outside [0, place_tr.len); in_ptrs[b*n_tracks+tr] are the (resampled)

@@ -145,10 +145,13 @@ const char *xmh_arch_name(void)
     return name;
 }
 
-int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches)
+int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
 {
     int rc = xmh_launch_mix_fast(j, stream, n_launches);
-    if (rc != XM_ENOSYS_) return rc;   // fast path took it (or failed for real)
+    if (rc != XM_ENOSYS_) {   // fast path took it (or failed for real)
+        if (!rc && n_fast) *n_fast += 1;
+        return rc;
+    }
     return xmh_launch_mix_generic(j, stream, n_launches);
 }
 

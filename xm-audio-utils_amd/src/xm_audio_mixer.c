@@ -26,6 +26,7 @@ struct XmAudioMixer {
     int user_stream;
     void *ev[6];
     XmMixerTiming timing;
+    int ev_done;                   /* this call recorded ev[2] then ev[3] (kernel window) */
     /* device scratch */
     void *d_in, *d_out, *d_fx;
     size_t d_in_cap, d_out_cap, d_fx_cap;
@@ -142,26 +143,56 @@ int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_
 {
     if (!m || !tracks || n_tracks < 1 || n_tracks > XM_MAX_TRACKS) return XM_EINVAL;
     XmhGain g[XM_MAX_TRACKS];
-    int trk_rt[XM_MAX_TRACKS], mixed = 0;
+    int trk_rt[XM_MAX_TRACKS], mixed = 0, rc = XM_OK;
     for (int i = 0; i < n_tracks; ++i) {
         if (tracks[i].in_rate < 0) return XM_EINVAL;
-        int rc = xm_gain_to_dev(&tracks[i].gain, &g[i]);
-        if (rc) return rc;
+        if ((rc = xm_gain_to_dev(&tracks[i].gain, &g[i]))) return rc;
+    }
+    /* per-track rate tables: the cache is rebuilt from this track list (kept
+     * tables move over, new rates are designed, rates no track uses any more
+     * are freed), so it never holds more than the distinct rates in use.  On
+     * failure the handle keeps its previous tracks and tables. */
+    XmTable nrt[XM_MAX_TRACKS];
+    int32_t nrate[XM_MAX_TRACKS];
+    int from_old[XM_MAX_TRACKS], nn = 0;
+    for (int i = 0; i < n_tracks && !rc; ++i) {
         trk_rt[i] = -1;
         const int32_t r = tracks[i].in_rate;
         if (r == 0 || r == m->cfg.in_rate) continue;
         mixed = 1;
         int k = 0;
-        while (k < m->n_rt && m->rt_rate[k] != r) ++k;
-        if (k == m->n_rt) {   /* a new rate: design its table once and keep it */
-            if (m->n_rt == XM_MAX_TRACKS) return XM_ENOMEM;
-            if ((rc = xmh_set_device(m->cfg.device))) return rc;
-            if ((rc = xm_table_build(&m->rt[k], r, m->cfg.out_rate))) return rc;
-            m->rt_rate[k] = r;
-            m->n_rt++;
+        while (k < nn && nrate[k] != r) ++k;
+        if (k == nn) {
+            int j = 0;
+            while (j < m->n_rt && m->rt_rate[j] != r) ++j;
+            if (j < m->n_rt) {
+                nrt[nn] = m->rt[j];
+                from_old[nn] = j;
+            } else {
+                if ((rc = xmh_set_device(m->cfg.device))) break;
+                if ((rc = xm_table_build(&nrt[nn], r, m->cfg.out_rate))) break;
+                from_old[nn] = -1;
+            }
+            nrate[nn++] = r;
         }
         trk_rt[i] = k;
     }
+    if (rc) {
+        for (int k = 0; k < nn; ++k)
+            if (from_old[k] < 0) xm_table_free(&nrt[k]);
+        return rc;
+    }
+    for (int j = 0; j < m->n_rt; ++j) {
+        int kept = 0;
+        for (int k = 0; k < nn; ++k) kept |= from_old[k] == j;
+        if (!kept) {
+            xmh_set_device(m->cfg.device);
+            xm_table_free(&m->rt[j]);
+        }
+    }
+    memcpy(m->rt, nrt, sizeof(XmTable) * (size_t)nn);
+    memcpy(m->rt_rate, nrate, sizeof(int32_t) * (size_t)nn);
+    m->n_rt = nn;
     memcpy(m->trk_rt, trk_rt, sizeof(int) * (size_t)n_tracks);
     m->mixed_rates = mixed;
     memcpy(m->tracks, tracks, sizeof(XmTrackDesc) * (size_t)n_tracks);
@@ -170,8 +201,7 @@ int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_
     m->gains_dirty = 1;
     const XmhGain *g0 = &g[0];
     int const_one = (g0->flags == 0) &&
-                    (m->cfg.sample_fmt == XM_FMT_F32 ? (g0->g0 == 1.0f && (g0->len == 0 ? g0->g1 == 1.0f
-                                                                                         : g0->g1 == 1.0f))
+                    (m->cfg.sample_fmt == XM_FMT_F32 ? (g0->g0 == 1.0f && g0->g1 == 1.0f)
                                                      : (g0->q0 == 32768 && g0->q1 == 32768));
     m->unity = n_tracks == 1 && const_one;
     return XM_OK;
@@ -226,6 +256,13 @@ int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t)
     if (!m || !t) return XM_EINVAL;
     *t = m->timing;
     return XM_OK;
+}
+
+/* every process-style call starts here: clears the timing of the last call */
+static void begin_call(XmAudioMixer *m)
+{
+    memset(&m->timing, 0, sizeof m->timing);
+    m->ev_done = 0;
 }
 
 /* ---- core: run one device-resident job ----------------------------------- */
@@ -303,7 +340,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     } else {
         rc = XM_ENOSYS;   /* irregular strides with effects: use process_batch */
     }
-    if (!rc) rc = xmh_launch_mix(&r, m->stream, launches);
+    if (!rc) rc = xmh_launch_mix(&r, m->stream, launches, &m->timing.fast_launches);
     /* 2) effects chain on every track, in insertion order */
     void **tmp_ptrs = NULL;
     int cur = 0;   /* 0: tracks in scratch, 1: in scratch2 */
@@ -353,7 +390,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         x.rs.rm = 0;
         x.unity = 0;
         x.rs.fast = 0;
-        rc = xmh_launch_mix(&x, m->stream, launches);
+        rc = xmh_launch_mix(&x, m->stream, launches, &m->timing.fast_launches);
     }
     xmh_stream_sync(m->stream);
     xmh_free(tmp_ptrs);
@@ -367,9 +404,10 @@ static int run_job(XmAudioMixer *m, XmhMixJob *j)
     int rc = xmh_event_record(m->ev[2], m->stream);
     if (rc) return rc;
     if (m->fx) rc = run_with_effects(m, j, &launches);
-    else rc = xmh_launch_mix(j, m->stream, &launches);
+    else rc = xmh_launch_mix(j, m->stream, &launches, &m->timing.fast_launches);
     int rc2 = xmh_event_record(m->ev[3], m->stream);
     m->timing.n_launches += launches;
+    if (!rc && !rc2) m->ev_done = 1;
     return rc ? rc : rc2;
 }
 
@@ -424,7 +462,7 @@ static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *
 static int finish(XmAudioMixer *m, int rc)
 {
     if (!rc && !m->user_stream) rc = xmh_stream_sync(m->stream);
-    if (!rc && !m->user_stream) {
+    if (!rc && !m->user_stream && m->ev_done) {   /* only events this call recorded */
         float ms = 0.0f;
         if (!xmh_event_elapsed(&ms, m->ev[2], m->ev[3])) m->timing.kernel_ms = ms;
     }
@@ -506,6 +544,7 @@ static int process_host(XmAudioMixer *m, const void *const *in, void *const *out
     m->timing.h2d_ms = h2d;
     m->timing.kernel_ms = ker;
     m->timing.d2h_ms = d2h;
+    m->ev_done = 0;   /* kernel_ms is the sum over chunks, not the last chunk's window */
     return rc;
 }
 
@@ -522,7 +561,7 @@ int xm_audio_mixer_process_batch(XmAudioMixer *m, const void *const *in, void *c
         if (!out[i]) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
-    memset(&m->timing, 0, sizeof m->timing);
+    begin_call(m);
     if ((rc = upload_gains(m))) return rc;
     if (xm_audio_mixer_out_frames(m, frames_in) == 0) return XM_OK;
     if (m->cfg.mem_kind == XM_MEM_DEVICE) rc = process_device(m, in, out, batch, frames_in);
@@ -542,7 +581,7 @@ int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in, ptrdiff_
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
-    memset(&m->timing, 0, sizeof m->timing);
+    begin_call(m);
     if ((rc = upload_gains(m))) return rc;
     if (xm_audio_mixer_out_frames(m, frames_in) == 0) return XM_OK;
     XmhMixJob j;
@@ -567,7 +606,7 @@ int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, int n_pa
     if (!partials || !out || batch > (size_t)INT32_MAX) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
-    memset(&m->timing, 0, sizeof m->timing);
+    begin_call(m);
     rc = xmh_event_record(m->ev[2], m->stream);
     if (!rc)
         rc = xmh_launch_finish_s16(partials, n_parts, part_stride, partial_mix_stride, out, out_mix_stride,
@@ -575,6 +614,7 @@ int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, int n_pa
     if (!rc) {
         m->timing.n_launches = 1;
         rc = xmh_event_record(m->ev[3], m->stream);
+        if (!rc) m->ev_done = 1;
     }
     return finish(m, rc);
 }
@@ -606,7 +646,7 @@ int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
-    memset(&m->timing, 0, sizeof m->timing);
+    begin_call(m);
     if ((rc = upload_gains(m))) return rc;
     if (xm_audio_mixer_out_frames(m, frames_in) == 0) return XM_OK;
     XmhMixJob j;
@@ -670,7 +710,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
 {
     if (frames_out) *frames_out = 0;
     if (!m || !m->st_on || (n && !in) || !frames_out) return XM_EINVAL;
-    if (m->fx) return XM_ENOSYS;
+    if (m->fx || m->mixed_rates) return XM_ENOSYS;   /* as stream_begin */
     if (m->n_tracks != m->st_ntr) return XM_EINVAL;   /* track list changed mid-stream */
     const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->st_ntr;
     const size_t batch = m->st_batch, rows = batch * (size_t)ntr, fb = (size_t)C * (size_t)elem;
@@ -682,7 +722,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     if (nout && (!out || out_cap < nout)) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
-    memset(&m->timing, 0, sizeof m->timing);
+    begin_call(m);
     if ((rc = upload_gains(m))) return rc;
     /* 1) append the block to the window */
     const size_t keep = (size_t)(m->st_recv - m->st_w0);
@@ -758,7 +798,9 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     }
     *frames_out = nout;
     if (flush) m->st_on = 0;
-    if (!nout) return m->cfg.mem_kind == XM_MEM_DEVICE || m->user_stream ? XM_OK : xmh_stream_sync(m->stream);
+    /* synchronous unless the caller installed a stream, whatever the block
+     * size: the window copies above read the caller's `in` asynchronously */
+    if (!nout) return m->user_stream ? XM_OK : xmh_stream_sync(m->stream);
     return finish(m, rc);
 }
 
@@ -844,7 +886,7 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
         j.rs.rm = t->d.rm;
         j.rs.H = t->H_dev;
         j.rs.fast = 0;
-        rc = xmh_launch_mix(&j, m->stream, &launches);
+        rc = xmh_launch_mix(&j, m->stream, &launches, &m->timing.fast_launches);
     }
     if (!rc) {
         XmhMixJob j;
@@ -862,6 +904,7 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
         rc = xmh_launch_mix_placed(&j, m->stream, &launches);
     }
     if (!rc) rc = xmh_event_record(m->ev[3], m->stream);
+    if (!rc) m->ev_done = 1;
     m->timing.n_launches += launches;
     return rc;
 }
@@ -882,7 +925,7 @@ int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, cons
         if (!out[i]) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
-    memset(&m->timing, 0, sizeof m->timing);
+    begin_call(m);
     if ((rc = upload_gains(m))) return rc;
     if (m->cfg.mem_kind == XM_MEM_DEVICE) return finish(m, timeline_device(m, in, place, out, batch, out_frames));
     /* host memory: stage one mix at a time */

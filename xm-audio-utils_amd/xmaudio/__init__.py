@@ -80,7 +80,7 @@ class XmMixerConfig(C.Structure):
 
 class XmMixerTiming(C.Structure):
     _fields_ = [("h2d_ms", C.c_float), ("kernel_ms", C.c_float), ("d2h_ms", C.c_float),
-                ("n_launches", C.c_int32), ("reserved", C.c_int32)]
+                ("n_launches", C.c_int32), ("fast_launches", C.c_int32)]
 
 
 class XmEffectsConfig(C.Structure):

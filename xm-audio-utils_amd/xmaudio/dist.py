@@ -1,8 +1,8 @@
 """Rank plumbing for multi-GPU runs.
 
 Mixes are independent, so N GPUs are N processes, each owning a contiguous
-block of mixes (weak scaling: a fixed block per rank) with no collective in
-the data path.  torch.distributed (RCCL = backend "nccl" on ROCm, or "gloo"
+block of mixes (bench.py: 4096 clips in total split over the ranks, strong
+scaling) with no collective in the data path.  torch.distributed (RCCL = backend "nccl" on ROCm, or "gloo"
 on CPU for tests) is used for the start/stop barriers and the max-over-ranks
 wall time, and for the one real exchange of the path: config 5
 (BASELINE.json:11), where the tracks of every mix are spread over the ranks
@@ -61,21 +61,42 @@ def reduce_partials(r: Rank, part):
     """Config 5 exchange.  `part` is this rank's [batch, S] int32 Q15 partial
     (xm_audio_mixer_process_partial_s16 over the tracks it holds); returns the
     [batch/world, S] block of the mixes owned_mixes() gives this rank, summed
-    over every rank.  int32 sums of <= 64 Q15 terms cannot overflow, so any
-    order is exact and RCCL's reduce-scatter (its own schedule over xGMI) is
-    bit-exact.  gloo (the CPU tests) gets the same block from an all-reduce."""
+    over every rank, from one reduce-scatter (RCCL over xGMI on GPUs, gloo in
+    the CPU tests: the same call on every backend).  int32 sums of <= 64 Q15
+    terms cannot overflow, so any order is exact and the collective's own
+    schedule cannot change a bit."""
     if r.world <= 1:
         return part
     import torch
     import torch.distributed as dist
-    first, n = owned_mixes(r, part.shape[0])
+    _, n = owned_mixes(r, part.shape[0])
     part = part.contiguous()
-    if dist.get_backend() == "gloo":
-        full = part.clone()
-        dist.all_reduce(full, op=dist.ReduceOp.SUM)
-        return full[first:first + n].contiguous()
     out = torch.empty((n,) + tuple(part.shape[1:]), dtype=part.dtype, device=part.device)
     dist.reduce_scatter_tensor(out, part, op=dist.ReduceOp.SUM)
+    return out
+
+
+def partial_s16(mixer, x):
+    """This rank's int32 partial of every mix: x [batch, tracks_here, frames, C]
+    int16 (mixer.set_tracks holds those tracks' ramps) -> [batch, out_frames*C]."""
+    import torch
+    B, T, F, C = x.shape
+    Fo = mixer.out_frames(F)
+    x = x.contiguous()
+    part = torch.empty((B, Fo * C), dtype=torch.int32, device=x.device)
+    mixer.process_partial_strided(x.data_ptr(), F * C, T * F * C, part.data_ptr(), Fo * C, B, F)
+    return part
+
+
+def finish_block_s16(mixer, blk, channels, out=None):
+    """Saturate a summed [n, out_frames*C] int32 block to [n, out_frames, C] int16."""
+    import torch
+    blk = blk.contiguous()
+    n, S = blk.shape
+    Fo = S // channels
+    if out is None:
+        out = torch.empty((n, Fo, channels), dtype=torch.int16, device=blk.device)
+    mixer.finish_s16(blk.data_ptr(), 1, 0, S, out.data_ptr(), S, n, Fo)
     return out
 
 
@@ -84,17 +105,8 @@ def mix_spanning_s16(r: Rank, mixer, x, out=None):
     this rank's tracks of every mix (mixer.set_tracks holds their ramps).
     Returns [batch/world, out_frames, C] int16: the finished mixes
     owned_mixes() gives this rank (partial -> reduce_partials -> finish)."""
-    import torch
-    B, T, F, C = x.shape
-    Fo = mixer.out_frames(F)
-    part = torch.empty((B, Fo * C), dtype=torch.int32, device=x.device)
-    mixer.process_partial_strided(x.data_ptr(), F * C, T * F * C, part.data_ptr(), Fo * C, B, F)
-    blk = reduce_partials(r, part)
-    n = blk.shape[0]
-    if out is None:
-        out = torch.empty((n, Fo, C), dtype=torch.int16, device=x.device)
-    mixer.finish_s16(blk.data_ptr(), 1, 0, Fo * C, out.data_ptr(), Fo * C, n, Fo)
-    return out
+    blk = reduce_partials(r, partial_s16(mixer, x))
+    return finish_block_s16(mixer, blk, x.shape[3], out)
 
 
 def barrier(r: Rank) -> None:
@@ -112,6 +124,17 @@ def max_over_ranks(r: Rank, value: float, device="cpu") -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def min_over_ranks(r: Rank, flag: bool, device="cpu") -> bool:
+    """True only if `flag` holds on every rank (the job's parity bit)."""
+    if r.world <= 1:
+        return bool(flag)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
 
 
 def finish(r: Rank) -> None:
