@@ -17,6 +17,19 @@
  * the caller installed a stream with xm_audio_mixer_set_stream(), in which
  * case DEVICE-memory calls are stream-ordered and return without waiting
  * (the cuBLAS/hipBLAS convention).
+ *
+ * Multi-device handles (SURVEY.md §8(b) n_devices, §8(e)): a handle created
+ * with XmMixerConfig.n_devices > 1 (devices device .. device+n-1) or by
+ * xm_audio_mixer_create_multi() (any device list) owns one single-device
+ * handle and one host worker thread per device.  A batch call splits its
+ * mixes into contiguous blocks, block d (the first batch % n blocks one mix
+ * longer) running on device d, and joins every worker before it returns;
+ * independent mixes need no exchange, so the result is the one-device result
+ * bit for bit.  Tracks that span devices (config 5) meet in one exchange
+ * inside xm_audio_mixer_mix_spanning_s16 (RCCL reduce-scatter over xGMI).
+ * On such a handle set_stream, process_partial_s16 and finish_s16 return
+ * XM_ENOSYS; DEVICE-memory batches go through process_batch (each block's
+ * pointers on its device) or process_sharded.
  */
 #ifndef XM_AUDIO_MIXER_H
 #define XM_AUDIO_MIXER_H
@@ -45,7 +58,7 @@ typedef struct XmMixerConfig {
     int32_t mem_kind;     /* XmMemKind of the in/out pointers */
     int32_t device;       /* HIP device ordinal the handle runs on */
     int32_t flags;        /* 0 or XM_MIXER_OUT_CONVERT */
-    int32_t reserved;
+    int32_t n_devices;    /* 0 or 1: one device; n > 1: devices device .. device+n-1 */
 } XmMixerConfig;
 
 typedef struct XmTrackDesc {
@@ -72,6 +85,15 @@ typedef struct XmMixerTiming {
  * is no CPU fallback in the product library. */
 XM_API XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status);
 XM_API XmAudioMixer *xm_audio_mixer_create(const XmMixerConfig *cfg);
+
+/* Multi-device handle over an explicit device list (n_devices in [1, 16];
+ * a device may appear more than once: two blocks on one GPU).  cfg->device
+ * and cfg->n_devices are ignored. */
+XM_API XmAudioMixer *xm_audio_mixer_create_multi(const XmMixerConfig *cfg, const int *devices, int n_devices,
+                                                 int *status);
+
+/* Devices a handle runs on (1 for a single-device handle). */
+XM_API int xm_audio_mixer_n_devices(const XmAudioMixer *m);
 
 /* Replace the track list (n_tracks in [1, 64]). */
 XM_API int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_tracks);
@@ -106,6 +128,14 @@ XM_API int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in,
                                    void *out, ptrdiff_t out_mix_stride,
                                    size_t batch, size_t frames_in);
 
+/* Multi-device handles, DEVICE memory already resident per device (the bench
+ * shape): in[d] / out[d] are device d's tracks and outputs, strided as
+ * process_strided, batch[d] its mixes (0 = idle).  A single-device handle
+ * takes n = 1 arrays. */
+XM_API int xm_audio_mixer_process_sharded(XmAudioMixer *m, const void *const *in, ptrdiff_t in_track_stride,
+                                          ptrdiff_t in_mix_stride, void *const *out, ptrdiff_t out_mix_stride,
+                                          const size_t *batch, size_t frames_in);
+
 /* ---- cross-device mixdown (BASELINE.json:11, config 5: the tracks of one mix
  * live on different devices).  Each device runs the tracks it holds through
  * process_partial_s16, which writes the Q15 track sum of every output sample
@@ -130,6 +160,21 @@ XM_API int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, i
                               ptrdiff_t part_stride, ptrdiff_t partial_mix_stride,
                               int16_t *out, ptrdiff_t out_mix_stride,
                               size_t batch, size_t out_frames);
+
+/* Config 5 inside the library, on a multi-device S16 / DEVICE-memory handle
+ * of n devices: the handle's n_tracks tracks are split evenly over the
+ * devices (n_tracks % n == 0), device d holding tracks [d*T/n, (d+1)*T/n) of
+ * every mix at in[d] (layout as process_strided over those T/n tracks).
+ * Every device forms the int32 partial of its tracks; the partials meet in
+ * one exchange -- an RCCL reduce-scatter over xGMI when the devices are
+ * distinct (communicator created on first use, ncclCommInitAll), device
+ * copies when a device repeats -- and device d saturates the mixes it owns,
+ * [d*batch/n, (d+1)*batch/n) (batch % n == 0), into out[d] (out_mix_stride
+ * apart).  Equal bit for bit to one 64-track process_* call.  XM_ECOMM if
+ * the exchange fails (RCCL absent or a communicator error). */
+XM_API int xm_audio_mixer_mix_spanning_s16(XmAudioMixer *m, const void *const *in, ptrdiff_t in_track_stride,
+                                           ptrdiff_t in_mix_stride, void *const *out, ptrdiff_t out_mix_stride,
+                                           size_t batch, size_t frames_in);
 
 /* ---- streaming (build-owned) ----------------------
  * `batch` mixes whose tracks arrive in blocks.  stream_begin() starts them at

@@ -10,11 +10,13 @@ import pytest
 from conftest import LIB_DIR, ROOT
 
 
-def _build(tmp_path, name="xm_mix_example"):
+def _build(tmp_path, name="xm_mix_example", hip=False):
     exe = tmp_path / name
-    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "examples", name + ".c"), "-L", LIB_DIR, "-lxm_audio",
-           f"-Wl,-rpath,{LIB_DIR}", "-lm", "-o", str(exe)]
+    extra = ["-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"] if hip else []
+    libs = ["-L", "/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"] if hip else []
+    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include")] + extra + \
+          [os.path.join(ROOT, "examples", name + ".c"), "-L", LIB_DIR, "-lxm_audio",
+           f"-Wl,-rpath,{LIB_DIR}"] + libs + ["-lm", "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     return exe
 
@@ -59,3 +61,23 @@ def test_stream_example_runs_on_gpu(tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     assert "bit-identical to process_batch" in p.stdout
     assert "timeline: 44100 frames" in p.stdout
+
+
+def test_multi_example_builds_and_refuses_without_gpu(tmp_path):
+    """The multi-device entry points (create_multi, process_strided over a
+    device list, mix_spanning_s16) compile from plain C11 (-Werror)."""
+    exe = _build(tmp_path, "xm_multi_example", hip=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    if "0 HIP device(s)" in p.stdout:
+        assert p.returncode == 2, p.stderr
+    else:
+        assert p.returncode == 0, p.stdout + p.stderr
+
+
+@pytest.mark.gpu
+def test_multi_example_runs_on_gpu(tmp_path):
+    exe = _build(tmp_path, "xm_multi_example", hip=True)
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "bit-identical to one device" in p.stdout
+    assert "config 5:" in p.stdout

@@ -125,6 +125,19 @@ void xmh_event_destroy(void *e);
 int  xmh_event_record(void *e, void *s);
 int  xmh_event_elapsed(float *ms, void *e0, void *e1);  /* syncs e1 */
 int  xmh_pointer_is_device(const void *p);     /* 1 device, 0 host, <0 error */
+/* device-to-device copy between (possibly different) devices, on stream s */
+int  xmh_memcpy_peer(void *dst, int dst_dev, const void *src, int src_dev, size_t bytes, void *s);
+
+/* ---------- RCCL (config 5 exchange), loaded on first use ------------------ */
+/* one communicator per device of devs (distinct ordinals), ncclCommInitAll */
+int  xmh_comm_init_all(void **comms, int n, const int *devs);
+void xmh_comm_destroy(void *comm);
+int  xmh_group_start(void);
+int  xmh_group_end(void);
+/* recv (recv_count int32) = block `rank` of the element-wise sum of every
+ * rank's send (n * recv_count int32); enqueued on stream s */
+int  xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s);
+int  xmh_comm_check(void *comm);               /* XM_ECOMM on an asynchronous error */
 const char *xmh_arch_name(void);
 
 /* ---------- kernels ----------------------------------------------------------- */

@@ -3,13 +3,16 @@
 // xm_shim.hip — the thin C-ABI shim (SURVEY.md §1 layer L1): HIP runtime
 // wrappers with every hipError_t mapped to an XM_* status, and the kernel
 // dispatch for mix / effects jobs.  Only the C host layer (src/*.c) calls it.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <string.h>
 #include "xm_shim.h"
 
 #define XM_EDEVICE_ (-1001)
 #define XM_ENOMEM_ (-12)
 #define XM_ENOSYS_ (-1003)
+#define XM_ECOMM_ (-1002)
 
 #define map(e) map_at((e), __LINE__)
 static inline int map_at(hipError_t e, int line)
@@ -133,6 +136,88 @@ int xmh_pointer_is_device(const void *p)
         return 0;   // unregistered host memory
     }
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ? 1 : 0;
+}
+
+int xmh_memcpy_peer(void *dst, int dst_dev, const void *src, int src_dev, size_t n, void *s)
+{
+    if (!n) return 0;
+    if (dst_dev == src_dev) return map(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)s));
+    return map(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, n, (hipStream_t)s));
+}
+
+// ---- RCCL, resolved with dlopen on first use: the library has no link-time
+// dependency on librccl, and a process that already loaded it (torch) shares
+// that copy.  Only config 5's exchange (xm_audio_mixer_mix_spanning_s16) uses it.
+}  // extern "C"
+namespace {
+struct Rccl {
+    bool tried = false, ok = false;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
+    decltype(&ncclGetErrorString) err_str = nullptr;
+};
+Rccl &rccl()
+{
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        if (getenv("XM_DEBUG")) fprintf(stderr, "xm_shim: librccl not found: %s\n", dlerror());
+        return r;
+    }
+    r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+    r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+    r.reduce_scatter = (decltype(r.reduce_scatter))dlsym(h, "ncclReduceScatter");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+    r.async_error = (decltype(r.async_error))dlsym(h, "ncclCommGetAsyncError");
+    r.err_str = (decltype(r.err_str))dlsym(h, "ncclGetErrorString");
+    r.ok = r.init_all && r.destroy && r.reduce_scatter && r.group_start && r.group_end && r.async_error;
+    return r;
+}
+int cmap(ncclResult_t e, int line)
+{
+    if (e == ncclSuccess) return 0;
+    if (getenv("XM_DEBUG"))
+        fprintf(stderr, "xm_shim.hip:%d: rccl %s\n", line, rccl().err_str ? rccl().err_str(e) : "error");
+    return XM_ECOMM_;
+}
+}  // namespace
+extern "C" {
+
+int xmh_comm_init_all(void **comms, int n, const int *devs)
+{
+    if (!rccl().ok) return XM_ECOMM_;
+    return cmap(rccl().init_all((ncclComm_t *)comms, n, devs), __LINE__);
+}
+
+void xmh_comm_destroy(void *comm)
+{
+    if (comm && rccl().ok) (void)rccl().destroy((ncclComm_t)comm);
+}
+
+int xmh_group_start(void) { return rccl().ok ? cmap(rccl().group_start(), __LINE__) : XM_ECOMM_; }
+int xmh_group_end(void) { return rccl().ok ? cmap(rccl().group_end(), __LINE__) : XM_ECOMM_; }
+
+int xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s)
+{
+    if (!rccl().ok) return XM_ECOMM_;
+    return cmap(rccl().reduce_scatter(send, recv, recv_count, ncclInt32, ncclSum, (ncclComm_t)comm, (hipStream_t)s),
+                __LINE__);
+}
+
+int xmh_comm_check(void *comm)
+{
+    if (!rccl().ok || !comm) return XM_ECOMM_;
+    ncclResult_t a = ncclSuccess;
+    int rc = cmap(rccl().async_error((ncclComm_t)comm, &a), __LINE__);
+    return rc ? rc : cmap(a, __LINE__);
 }
 
 const char *xmh_arch_name(void)

@@ -49,7 +49,16 @@ struct XmAudioMixer {
     int trk_rt[XM_MAX_TRACKS];
     int64_t *place_dev;            /* [XM_MAX_TRACKS][2] */
     XmhGain *unity_dev;            /* one unity-gain descriptor */
+    XmMulti *multi;                /* multi-device handle: every call dispatches here */
 };
+
+void *xm_mixer_stream(const XmAudioMixer *m) { return m->stream; }
+
+const XmTrackDesc *xm_mixer_tracks(const XmAudioMixer *m, int *n_tracks)
+{
+    *n_tracks = m->n_tracks;
+    return m->tracks;
+}
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
 
@@ -73,16 +82,62 @@ static int grow(void **p, size_t *cap, size_t need)
     return XM_OK;
 }
 
+static int cfg_valid(const XmMixerConfig *cfg)
+{
+    return cfg && cfg->in_rate > 0 && cfg->out_rate > 0 && (cfg->channels == 1 || cfg->channels == 2) &&
+           (cfg->sample_fmt == XM_FMT_S16 || cfg->sample_fmt == XM_FMT_F32) &&
+           (cfg->mem_kind == XM_MEM_HOST || cfg->mem_kind == XM_MEM_DEVICE) && cfg->device >= 0 &&
+           !(cfg->flags & ~(int32_t)XM_MIXER_OUT_CONVERT) && cfg->n_devices >= 0 &&
+           cfg->n_devices <= XM_MAX_DEVICES;
+}
+
+XmAudioMixer *xm_audio_mixer_create_multi(const XmMixerConfig *cfg, const int *devices, int n_devices, int *status)
+{
+    int rc = XM_OK;
+    XmAudioMixer *m = NULL;
+    XmMixerConfig c;
+    if (!cfg || !devices || n_devices < 1 || n_devices > XM_MAX_DEVICES) {
+        rc = XM_EINVAL;
+        goto out;
+    }
+    c = *cfg;
+    c.device = devices[0];
+    c.n_devices = n_devices;
+    if (!cfg_valid(&c)) {
+        rc = XM_EINVAL;
+        goto out;
+    }
+    for (int d = 0; d < n_devices; ++d)
+        if (devices[d] < 0 || devices[d] >= xmh_device_count()) {
+            rc = devices[d] < 0 ? XM_EINVAL : XM_EDEVICE;
+            goto out;
+        }
+    m = calloc(1, sizeof *m);
+    if (!m) {
+        rc = XM_ENOMEM;
+        goto out;
+    }
+    m->cfg = c;
+    m->multi = xm_multi_create(&c, devices, n_devices, &rc);
+    if (!rc) m->n_tracks = 1;
+out:
+    if (rc) xm_audio_mixer_freep(&m);
+    if (status) *status = rc;
+    return m;
+}
+
 XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status)
 {
     int rc = XM_OK;
     XmAudioMixer *m = NULL;
-    if (!cfg || cfg->in_rate <= 0 || cfg->out_rate <= 0 || (cfg->channels != 1 && cfg->channels != 2) ||
-        (cfg->sample_fmt != XM_FMT_S16 && cfg->sample_fmt != XM_FMT_F32) ||
-        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) || cfg->device < 0 ||
-        (cfg->flags & ~(int32_t)XM_MIXER_OUT_CONVERT)) {
+    if (!cfg_valid(cfg)) {
         rc = XM_EINVAL;
         goto out;
+    }
+    if (cfg->n_devices > 1) {   /* devices device .. device+n-1 */
+        int devs[XM_MAX_DEVICES];
+        for (int d = 0; d < cfg->n_devices; ++d) devs[d] = cfg->device + d;
+        return xm_audio_mixer_create_multi(cfg, devs, cfg->n_devices, status);
     }
     if (cfg->device >= xmh_device_count()) {
         rc = XM_EDEVICE;
@@ -119,6 +174,12 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
 {
     if (!pm || !*pm) return;
     XmAudioMixer *m = *pm;
+    if (m->multi || m->cfg.n_devices > 1) {   /* the sub-handles own every device resource */
+        xm_multi_free(m->multi);
+        free(m);
+        *pm = NULL;
+        return;
+    }
     xmh_set_device(m->cfg.device);
     if (m->own_stream) xmh_stream_sync(m->own_stream);
     xm_table_free(&m->table);
@@ -142,6 +203,11 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
 int xm_audio_mixer_set_tracks(XmAudioMixer *m, const XmTrackDesc *tracks, int n_tracks)
 {
     if (!m || !tracks || n_tracks < 1 || n_tracks > XM_MAX_TRACKS) return XM_EINVAL;
+    if (m->multi) {
+        int rc = xm_multi_set_tracks(m->multi, tracks, n_tracks);
+        if (!rc) m->n_tracks = n_tracks;
+        return rc;
+    }
     XmhGain g[XM_MAX_TRACKS];
     int trk_rt[XM_MAX_TRACKS], mixed = 0, rc = XM_OK;
     for (int i = 0; i < n_tracks; ++i) {
@@ -211,6 +277,7 @@ int xm_audio_mixer_set_crossfade(XmAudioMixer *m, int from, int to, int64_t star
 {
     if (!m || from < 0 || to < 0 || from >= m->n_tracks || to >= m->n_tracks || from == to || len < 0)
         return XM_EINVAL;
+    if (m->multi) return xm_multi_set_crossfade(m->multi, from, to, start, len);
     XmTrackDesc t[XM_MAX_TRACKS];
     memcpy(t, m->tracks, sizeof(XmTrackDesc) * (size_t)m->n_tracks);
     t[from].gain.mode = XM_GAIN_XFADE_OUT;
@@ -229,6 +296,10 @@ int xm_audio_mixer_set_crossfade(XmAudioMixer *m, int from, int to, int64_t star
 int xm_audio_mixer_set_track_effects(XmAudioMixer *m, const XmEffects *fx)
 {
     if (!m) return XM_EINVAL;
+    if (m->multi) {
+        if (fx && m->cfg.sample_fmt != XM_FMT_F32) return XM_ENOSYS;
+        return xm_multi_set_track_effects(m->multi, fx);
+    }
     if (fx) {
         if (m->cfg.sample_fmt != XM_FMT_F32) return XM_ENOSYS;
         if (xm_effects_device(fx) != m->cfg.device) return XM_EINVAL;
@@ -246,14 +317,22 @@ size_t xm_audio_mixer_out_frames(const XmAudioMixer *m, size_t frames_in)
 int xm_audio_mixer_set_stream(XmAudioMixer *m, void *s)
 {
     if (!m) return XM_EINVAL;
+    if (m->multi) return XM_ENOSYS;   /* a HIP stream belongs to one device */
     m->stream = s ? s : m->own_stream;
     m->user_stream = s != NULL;
     return XM_OK;
 }
 
+int xm_audio_mixer_n_devices(const XmAudioMixer *m)
+{
+    if (!m) return XM_EINVAL;
+    return m->multi ? xm_multi_n_devices(m->multi) : 1;
+}
+
 int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t)
 {
     if (!m || !t) return XM_EINVAL;
+    if (m->multi) return xm_multi_get_timing(m->multi, t);
     *t = m->timing;
     return XM_OK;
 }
@@ -555,6 +634,7 @@ int xm_audio_mixer_process_batch(XmAudioMixer *m, const void *const *in, void *c
     if (!m || (batch && (!in || !out))) return XM_EINVAL;
     if (batch == 0) return XM_OK;
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    if (m->multi) return xm_multi_process_batch(m->multi, in, out, batch, frames_in);
     for (size_t i = 0; i < batch * (size_t)m->n_tracks; ++i)
         if (!in[i]) return XM_EINVAL;
     for (size_t i = 0; i < batch; ++i)
@@ -574,6 +654,7 @@ int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in, ptrdiff_
                                        size_t batch, size_t frames_in)
 {
     if (!m || (batch && (!in || !partial))) return XM_EINVAL;
+    if (m->multi) return XM_ENOSYS;   /* config 5 on several devices: mix_spanning_s16 */
     if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx || m->mixed_rates ||
         (m->cfg.flags & XM_MIXER_OUT_CONVERT))
         return XM_ENOSYS;
@@ -601,7 +682,7 @@ int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, int n_pa
                               size_t out_frames)
 {
     if (!m || n_parts < 1 || n_parts > XM_MAX_TRACKS) return XM_EINVAL;
-    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE) return XM_ENOSYS;
+    if (m->multi || m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE) return XM_ENOSYS;
     if (batch == 0 || out_frames == 0) return XM_OK;
     if (!partials || !out || batch > (size_t)INT32_MAX) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
@@ -626,6 +707,8 @@ int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in
     if (m && m->mixed_rates) return XM_ENOSYS;   /* tracks of other rates: process_timeline */
     if (!m || (batch && (!in || !out))) return XM_EINVAL;
     if (batch == 0) return XM_OK;
+    if (m->multi) return xm_multi_process_strided(m->multi, in, in_track_stride, in_mix_stride, out, out_mix_stride,
+                                                  batch, frames_in);
     if (m->cfg.mem_kind != XM_MEM_DEVICE) {
         /* host memory: expand to pointer arrays */
         const int elem = fmt_bytes(m->cfg.sample_fmt);
@@ -687,6 +770,7 @@ static int64_t st_first_needed(const XmAudioMixer *m, int64_t mo)
 int xm_audio_mixer_stream_begin(XmAudioMixer *m, size_t batch)
 {
     if (!m || batch == 0 || batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
+    if (m->multi) return xm_multi_stream_begin(m->multi, batch);
     if (m->fx || m->mixed_rates) return XM_ENOSYS;   /* effects: xm_effects_process_stream */
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
@@ -700,6 +784,7 @@ int xm_audio_mixer_stream_begin(XmAudioMixer *m, size_t batch)
 
 size_t xm_audio_mixer_stream_out_frames(const XmAudioMixer *m, size_t frames_in, int flush)
 {
+    if (m && m->multi) return xm_multi_stream_out_frames(m->multi, frames_in, flush);
     if (!m || !m->st_on) return 0;
     int64_t e = st_ready_out(m, m->st_recv + (int64_t)frames_in, flush);
     return e > m->st_out ? (size_t)(e - m->st_out) : 0;
@@ -709,6 +794,10 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
                    ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush)
 {
     if (frames_out) *frames_out = 0;
+    if (m && m->multi) {
+        if ((n && !in) || !frames_out) return XM_EINVAL;
+        return xm_multi_stream_step(m->multi, in, ts, ms, n, out, os, out_cap, frames_out, flush);
+    }
     if (!m || !m->st_on || (n && !in) || !frames_out) return XM_EINVAL;
     if (m->fx || m->mixed_rates) return XM_ENOSYS;   /* as stream_begin */
     if (m->n_tracks != m->st_ntr) return XM_EINVAL;   /* track list changed mid-stream */
@@ -915,6 +1004,7 @@ int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, cons
     if (!m || !place || (batch && (!in || !out))) return XM_EINVAL;
     if (m->fx) return XM_ENOSYS;
     if (batch == 0 || out_frames == 0) return XM_OK;
+    if (m->multi) return xm_multi_process_timeline(m->multi, in, place, out, batch, out_frames);
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
     const int ntr = m->n_tracks;
     for (int tr = 0; tr < ntr; ++tr)
@@ -952,4 +1042,34 @@ int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, cons
         if (!rc) rc = xmh_stream_sync(m->stream);
     }
     return finish(m, rc);
+}
+
+/* ---- multi-device entry points (src/xm_mixer_multi.c) -------------------- */
+int xm_audio_mixer_process_sharded(XmAudioMixer *m, const void *const *in, ptrdiff_t in_track_stride,
+                                   ptrdiff_t in_mix_stride, void *const *out, ptrdiff_t out_mix_stride,
+                                   const size_t *batch, size_t frames_in)
+{
+    if (!m || !in || !out || !batch) return XM_EINVAL;
+    if (m->multi)
+        return xm_multi_process_sharded(m->multi, in, in_track_stride, in_mix_stride, out, out_mix_stride, batch,
+                                        frames_in);
+    if (m->cfg.mem_kind != XM_MEM_DEVICE) return XM_EINVAL;
+    return xm_audio_mixer_process_strided(m, in[0], in_track_stride, in_mix_stride, out[0], out_mix_stride, batch[0],
+                                          frames_in);
+}
+
+int xm_audio_mixer_mix_spanning_s16(XmAudioMixer *m, const void *const *in, ptrdiff_t in_track_stride,
+                                    ptrdiff_t in_mix_stride, void *const *out, ptrdiff_t out_mix_stride, size_t batch,
+                                    size_t frames_in)
+{
+    if (!m || !in || !out) return XM_EINVAL;
+    if (m->fx || m->mixed_rates) return XM_ENOSYS;
+    if (m->multi)
+        return xm_multi_mix_spanning_s16(m->multi, in, in_track_stride, in_mix_stride, out, out_mix_stride, batch,
+                                         frames_in);
+    /* one device holds every track: no exchange, the plain mix */
+    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || (m->cfg.flags & XM_MIXER_OUT_CONVERT))
+        return XM_ENOSYS;
+    return xm_audio_mixer_process_strided(m, in[0], in_track_stride, in_mix_stride, out[0], out_mix_stride, batch,
+                                          frames_in);
 }

@@ -208,6 +208,20 @@ int xm_effects_set_stream(XmEffects *e, void *s)
 
 int xm_effects_device(const XmEffects *e) { return e ? e->cfg.device : -1; }
 
+XmEffects *xm_effects_clone_on(const XmEffects *src, int device, int *status)
+{
+    XmEffectsConfig c = src->cfg;
+    c.device = device;
+    int rc = XM_OK;
+    XmEffects *e = xm_effects_create_ex(&c, &rc);
+    for (int i = 0; e && !rc && i < src->n_effects; ++i)
+        rc = src->fx[i].kind == 1 ? xm_effects_add_biquad(e, src->fx[i].sos)
+                                  : xm_effects_add_fir(e, src->fx[i].fir, src->fx[i].n);
+    if (rc) xm_effects_freep(&e);
+    if (status) *status = rc;
+    return e;
+}
+
 /* Group consecutive biquads into cascades (<= XM_MAX_SOS sections each) and
  * upload coefficients. */
 static int build_stages(XmEffects *e)

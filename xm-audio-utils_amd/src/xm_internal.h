@@ -36,5 +36,36 @@ typedef struct XmFxStage {
 
 int xm_effects_stages(const XmEffects *e, const XmFxStage **stages, int *n_stages);
 int xm_effects_device(const XmEffects *e);
+/* the same chain (host coefficient copies replayed) on another device */
+XmEffects *xm_effects_clone_on(const XmEffects *src, int device, int *status);
+
+/* ---- multi-device mixer handles (src/xm_mixer_multi.c) ----------------- */
+#define XM_MAX_DEVICES 16
+typedef struct XmMulti XmMulti;
+/* one single-device sub-handle per entry of devs (duplicates allowed) */
+XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *status);
+void xm_multi_free(XmMulti *mu);
+int  xm_multi_n_devices(const XmMulti *mu);
+int  xm_multi_set_tracks(XmMulti *mu, const XmTrackDesc *tracks, int n_tracks);
+int  xm_multi_set_crossfade(XmMulti *mu, int from, int to, int64_t start, int64_t len);
+int  xm_multi_set_track_effects(XmMulti *mu, const XmEffects *fx);
+int  xm_multi_get_timing(const XmMulti *mu, XmMixerTiming *t);
+int  xm_multi_process_batch(XmMulti *mu, const void *const *in, void *const *out, size_t batch, size_t frames_in);
+int  xm_multi_process_strided(XmMulti *mu, const void *in, ptrdiff_t ts, ptrdiff_t ms, void *out, ptrdiff_t os,
+                              size_t batch, size_t frames_in);
+int  xm_multi_process_sharded(XmMulti *mu, const void *const *in, ptrdiff_t ts, ptrdiff_t ms, void *const *out,
+                              ptrdiff_t os, const size_t *batch, size_t frames_in);
+int  xm_multi_process_timeline(XmMulti *mu, const void *const *in, const XmTrackPlacement *place,
+                               void *const *out, size_t batch, size_t out_frames);
+int  xm_multi_stream_begin(XmMulti *mu, size_t batch);
+size_t xm_multi_stream_out_frames(const XmMulti *mu, size_t frames_in, int flush);
+int  xm_multi_stream_step(XmMulti *mu, const void *in, ptrdiff_t ts, ptrdiff_t ms, size_t n, void *out,
+                          ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush);
+int  xm_multi_mix_spanning_s16(XmMulti *mu, const void *const *in, ptrdiff_t ts, ptrdiff_t ms, void *const *out,
+                               ptrdiff_t os, size_t batch, size_t frames_in);
+/* the stream a single-device handle launches on (its own or the caller's) */
+void *xm_mixer_stream(const XmAudioMixer *m);
+/* a single-device handle's current track list */
+const XmTrackDesc *xm_mixer_tracks(const XmAudioMixer *m, int *n_tracks);
 
 #endif

@@ -1,0 +1,532 @@
+/*
+ * xm_mixer_multi.c — multi-device mixer handles (SURVEY.md §8(b) n_devices:
+ * "a handle spawns one host worker thread per GPU, joined before
+ * process_batch returns"; §8(e) partitioning).
+ *
+ * A multi-device handle owns one single-device handle (the whole single-GPU
+ * path: staging, kernels, streams) and one persistent host worker thread per
+ * device.  Mixes are independent, so a batch is cut into contiguous blocks,
+ * block d on device d, and no data crosses devices: the result is the
+ * one-device result bit for bit.  Config 5 (BASELINE.json:11), where the
+ * tracks of every mix live on different devices, is the one exchange: int32
+ * Q15 partials per device, one RCCL reduce-scatter over xGMI (or device
+ * copies + an ordered sum when a device appears twice in the list), and a
+ * saturating finish on the device that owns each block of mixes.  int32 sums
+ * of <= 64 Q15 terms are exact in any order, so the
+ * collective's schedule cannot change a bit.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "xm_internal.h"
+
+typedef int (*XmTask)(XmMulti *mu, int d, void *arg);
+
+typedef struct XmWorker {
+    XmMulti *mu;
+    int d;
+} XmWorker;
+
+struct XmMulti {
+    int n;
+    int devs[XM_MAX_DEVICES];
+    XmAudioMixer *sub[XM_MAX_DEVICES];
+    XmEffects *fx[XM_MAX_DEVICES];     /* per-device clones of the track effects chain */
+    XmMixerConfig cfg;
+    int n_tracks;
+    XmTrackDesc tracks[XM_MAX_TRACKS]; /* the handle's full track list */
+    int span_mode;                     /* subs hold their config-5 track subsets */
+    /* worker pool (n > 1): worker d runs task(mu, d, arg) once per dispatch */
+    pthread_t th[XM_MAX_DEVICES];
+    XmWorker wk[XM_MAX_DEVICES];
+    int n_threads;
+    pthread_mutex_t lock;
+    pthread_cond_t go, done;
+    unsigned long gen;
+    int pending, quit;
+    XmTask task;
+    void *arg;
+    int rc[XM_MAX_DEVICES];
+    /* streaming: the block of mixes each device streams */
+    size_t st_first[XM_MAX_DEVICES], st_cnt[XM_MAX_DEVICES];
+    int st_on;
+    /* config 5 exchange */
+    int distinct;                      /* every device ordinal differs: RCCL */
+    void *comm[XM_MAX_DEVICES];
+    int comm_ready;
+    void *part[XM_MAX_DEVICES], *recv[XM_MAX_DEVICES];
+    size_t part_cap[XM_MAX_DEVICES], recv_cap[XM_MAX_DEVICES];
+};
+
+/* ---- worker pool -------------------------------------------------------- */
+static void *worker_main(void *p)
+{
+    XmWorker *w = p;
+    XmMulti *mu = w->mu;
+    unsigned long seen = 0;
+    pthread_mutex_lock(&mu->lock);
+    for (;;) {
+        while (!mu->quit && mu->gen == seen) pthread_cond_wait(&mu->go, &mu->lock);
+        if (mu->quit) break;
+        seen = mu->gen;
+        XmTask t = mu->task;
+        void *a = mu->arg;
+        pthread_mutex_unlock(&mu->lock);
+        int rc = t(mu, w->d, a);
+        pthread_mutex_lock(&mu->lock);
+        mu->rc[w->d] = rc;
+        if (--mu->pending == 0) pthread_cond_signal(&mu->done);
+    }
+    pthread_mutex_unlock(&mu->lock);
+    return NULL;
+}
+
+/* run task on every device (device d on worker d) and join; the first failing
+ * device's status (in device order) is returned */
+static int run_all(XmMulti *mu, XmTask t, void *arg)
+{
+    if (mu->n_threads == 0) {
+        for (int d = 0; d < mu->n; ++d) mu->rc[d] = t(mu, d, arg);
+    } else {
+        pthread_mutex_lock(&mu->lock);
+        mu->task = t;
+        mu->arg = arg;
+        mu->pending = mu->n;
+        mu->gen++;
+        pthread_cond_broadcast(&mu->go);
+        while (mu->pending) pthread_cond_wait(&mu->done, &mu->lock);
+        pthread_mutex_unlock(&mu->lock);
+    }
+    for (int d = 0; d < mu->n; ++d)
+        if (mu->rc[d]) return mu->rc[d];
+    return XM_OK;
+}
+
+/* contiguous block of `batch` mixes for device d: the first batch % n blocks
+ * hold one mix more */
+static void block(size_t batch, int n, int d, size_t *first, size_t *cnt)
+{
+    const size_t q = batch / (size_t)n, r = batch % (size_t)n;
+    *first = (size_t)d * q + ((size_t)d < r ? (size_t)d : r);
+    *cnt = q + ((size_t)d < r ? 1 : 0);
+}
+
+static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
+
+static int out_elem(const XmMixerConfig *c)
+{
+    const int conv = (c->flags & XM_MIXER_OUT_CONVERT) != 0;
+    return fmt_bytes(conv ? (c->sample_fmt == XM_FMT_S16 ? XM_FMT_F32 : XM_FMT_S16) : c->sample_fmt);
+}
+
+/* ---- lifecycle ------------------------------------------------------------ */
+XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *status)
+{
+    int rc = XM_OK;
+    XmMulti *mu = calloc(1, sizeof *mu);
+    if (!mu) {
+        if (status) *status = XM_ENOMEM;
+        return NULL;
+    }
+    mu->n = n;
+    mu->cfg = *cfg;
+    mu->cfg.n_devices = 0;
+    pthread_mutex_init(&mu->lock, NULL);
+    pthread_cond_init(&mu->go, NULL);
+    pthread_cond_init(&mu->done, NULL);
+    mu->distinct = 1;
+    for (int d = 0; d < n; ++d) {
+        mu->devs[d] = devs[d];
+        for (int e = 0; e < d; ++e) mu->distinct &= devs[e] != devs[d];
+    }
+    for (int d = 0; d < n && !rc; ++d) {
+        XmMixerConfig c = mu->cfg;
+        c.device = devs[d];
+        mu->sub[d] = xm_audio_mixer_create_ex(&c, &rc);
+    }
+    if (!rc) {   /* the handle's default track list: one unity track (as create_ex) */
+        memset(&mu->tracks[0], 0, sizeof mu->tracks[0]);
+        mu->tracks[0].gain.gain0 = mu->tracks[0].gain.gain1 = 1.0f;
+        mu->tracks[0].gain.gain0_q15 = mu->tracks[0].gain.gain1_q15 = 32768;
+        mu->n_tracks = 1;
+    }
+    for (int d = 0; d < n && !rc && n > 1; ++d) {
+        mu->wk[d].mu = mu;
+        mu->wk[d].d = d;
+        if (pthread_create(&mu->th[d], NULL, worker_main, &mu->wk[d])) rc = XM_ENOMEM;
+        else mu->n_threads++;
+    }
+    if (rc) {
+        xm_multi_free(mu);
+        mu = NULL;
+    }
+    if (status) *status = rc;
+    return mu;
+}
+
+void xm_multi_free(XmMulti *mu)
+{
+    if (!mu) return;
+    pthread_mutex_lock(&mu->lock);
+    mu->quit = 1;
+    pthread_cond_broadcast(&mu->go);
+    pthread_mutex_unlock(&mu->lock);
+    for (int d = 0; d < mu->n_threads; ++d) pthread_join(mu->th[d], NULL);
+    for (int d = 0; d < mu->n; ++d) {
+        if (mu->comm[d]) xmh_comm_destroy(mu->comm[d]);
+        xmh_set_device(mu->devs[d]);
+        xmh_free(mu->part[d]);
+        xmh_free(mu->recv[d]);
+        xm_audio_mixer_freep(&mu->sub[d]);
+        xm_effects_freep(&mu->fx[d]);
+    }
+    pthread_cond_destroy(&mu->go);
+    pthread_cond_destroy(&mu->done);
+    pthread_mutex_destroy(&mu->lock);
+    free(mu);
+}
+
+int xm_multi_n_devices(const XmMulti *mu) { return mu->n; }
+
+/* ---- track list --------------------------------------------------------------
+ * Every sub-handle holds the full list, except while config 5 runs: then sub
+ * d holds its own tracks [d*T/n, (d+1)*T/n) (span_mode) until the next call
+ * that needs the full list. */
+static int set_full(XmMulti *mu)
+{
+    int rc = XM_OK;
+    for (int d = 0; d < mu->n && !rc; ++d) rc = xm_audio_mixer_set_tracks(mu->sub[d], mu->tracks, mu->n_tracks);
+    if (!rc) mu->span_mode = 0;
+    return rc;
+}
+
+static int ensure_full(XmMulti *mu) { return mu->span_mode ? set_full(mu) : XM_OK; }
+
+int xm_multi_set_tracks(XmMulti *mu, const XmTrackDesc *tracks, int n_tracks)
+{
+    /* validate on the first sub-handle; the others see the same list */
+    int rc = xm_audio_mixer_set_tracks(mu->sub[0], tracks, n_tracks);
+    if (rc) return rc;
+    memcpy(mu->tracks, tracks, sizeof(XmTrackDesc) * (size_t)n_tracks);
+    mu->n_tracks = n_tracks;
+    mu->span_mode = 1;   /* forces set_full over every sub */
+    return set_full(mu);
+}
+
+int xm_multi_set_crossfade(XmMulti *mu, int from, int to, int64_t start, int64_t len)
+{
+    int rc = ensure_full(mu);
+    if (rc) return rc;
+    if ((rc = xm_audio_mixer_set_crossfade(mu->sub[0], from, to, start, len))) return rc;
+    /* sub 0 now holds the new list: give it to the others */
+    int n = 0;
+    const XmTrackDesc *t = xm_mixer_tracks(mu->sub[0], &n);
+    memcpy(mu->tracks, t, sizeof(XmTrackDesc) * (size_t)n);
+    mu->n_tracks = n;
+    mu->span_mode = 1;
+    return set_full(mu);
+}
+
+int xm_multi_set_track_effects(XmMulti *mu, const XmEffects *fx)
+{
+    int rc = XM_OK;
+    for (int d = 0; d < mu->n && !rc; ++d) rc = xm_audio_mixer_set_track_effects(mu->sub[d], NULL);
+    for (int d = 0; d < mu->n; ++d) xm_effects_freep(&mu->fx[d]);
+    if (rc || !fx) return rc;
+    /* one copy of the chain per device (the coefficients live in its HBM) */
+    for (int d = 0; d < mu->n && !rc; ++d) {
+        mu->fx[d] = xm_effects_clone_on(fx, mu->devs[d], &rc);
+        if (!rc) rc = xm_audio_mixer_set_track_effects(mu->sub[d], mu->fx[d]);
+    }
+    if (rc)
+        for (int d = 0; d < mu->n; ++d) {
+            xm_audio_mixer_set_track_effects(mu->sub[d], NULL);
+            xm_effects_freep(&mu->fx[d]);
+        }
+    return rc;
+}
+
+int xm_multi_get_timing(const XmMulti *mu, XmMixerTiming *t)
+{
+    memset(t, 0, sizeof *t);
+    for (int d = 0; d < mu->n; ++d) {   /* devices run concurrently: the slowest one's times */
+        XmMixerTiming s;
+        xm_audio_mixer_get_timing(mu->sub[d], &s);
+        if (s.h2d_ms > t->h2d_ms) t->h2d_ms = s.h2d_ms;
+        if (s.kernel_ms > t->kernel_ms) t->kernel_ms = s.kernel_ms;
+        if (s.d2h_ms > t->d2h_ms) t->d2h_ms = s.d2h_ms;
+        t->n_launches += s.n_launches;
+        t->fast_launches += s.fast_launches;
+    }
+    return XM_OK;
+}
+
+/* ---- batch calls: block d on device d ------------------------------------ */
+typedef struct {
+    const void *const *in;
+    void *const *out;
+    const void *in1;
+    void *out1;
+    ptrdiff_t ts, ms, os;
+    size_t batch, frames;
+    const XmTrackPlacement *place;
+} XmBatchArg;
+
+static int t_batch(XmMulti *mu, int d, void *p)
+{
+    const XmBatchArg *a = p;
+    size_t f, c;
+    block(a->batch, mu->n, d, &f, &c);
+    if (!c) return XM_OK;
+    return xm_audio_mixer_process_batch(mu->sub[d], a->in + f * (size_t)mu->n_tracks, a->out + f, c, a->frames);
+}
+
+int xm_multi_process_batch(XmMulti *mu, const void *const *in, void *const *out, size_t batch, size_t frames_in)
+{
+    int rc = ensure_full(mu);
+    if (rc) return rc;
+    XmBatchArg a = {.in = in, .out = out, .batch = batch, .frames = frames_in};
+    return run_all(mu, t_batch, &a);
+}
+
+static int t_strided(XmMulti *mu, int d, void *p)
+{
+    const XmBatchArg *a = p;
+    size_t f, c;
+    block(a->batch, mu->n, d, &f, &c);
+    if (!c) return XM_OK;
+    const char *in = (const char *)a->in1 + (ptrdiff_t)f * a->ms * fmt_bytes(mu->cfg.sample_fmt);
+    char *out = (char *)a->out1 + (ptrdiff_t)f * a->os * out_elem(&mu->cfg);
+    return xm_audio_mixer_process_strided(mu->sub[d], in, a->ts, a->ms, out, a->os, c, a->frames);
+}
+
+int xm_multi_process_strided(XmMulti *mu, const void *in, ptrdiff_t ts, ptrdiff_t ms, void *out, ptrdiff_t os,
+                             size_t batch, size_t frames_in)
+{
+    /* one base pointer cannot address HBM of several devices */
+    if (mu->cfg.mem_kind == XM_MEM_DEVICE) return XM_EINVAL;
+    int rc = ensure_full(mu);
+    if (rc) return rc;
+    XmBatchArg a = {.in1 = in, .out1 = out, .ts = ts, .ms = ms, .os = os, .batch = batch, .frames = frames_in};
+    return run_all(mu, t_strided, &a);
+}
+
+typedef struct {
+    const void *const *in;
+    void *const *out;
+    ptrdiff_t ts, ms, os;
+    const size_t *batch;
+    size_t frames;
+} XmShardArg;
+
+static int t_sharded(XmMulti *mu, int d, void *p)
+{
+    const XmShardArg *a = p;
+    if (!a->batch[d]) return XM_OK;
+    return xm_audio_mixer_process_strided(mu->sub[d], a->in[d], a->ts, a->ms, a->out[d], a->os, a->batch[d],
+                                          a->frames);
+}
+
+int xm_multi_process_sharded(XmMulti *mu, const void *const *in, ptrdiff_t ts, ptrdiff_t ms, void *const *out,
+                             ptrdiff_t os, const size_t *batch, size_t frames_in)
+{
+    int rc = ensure_full(mu);
+    if (rc) return rc;
+    XmShardArg a = {in, out, ts, ms, os, batch, frames_in};
+    return run_all(mu, t_sharded, &a);
+}
+
+static int t_timeline(XmMulti *mu, int d, void *p)
+{
+    const XmBatchArg *a = p;
+    size_t f, c;
+    block(a->batch, mu->n, d, &f, &c);
+    if (!c) return XM_OK;
+    return xm_audio_mixer_process_timeline(mu->sub[d], a->in + f * (size_t)mu->n_tracks, a->place, a->out + f, c,
+                                           a->frames);
+}
+
+int xm_multi_process_timeline(XmMulti *mu, const void *const *in, const XmTrackPlacement *place, void *const *out,
+                              size_t batch, size_t out_frames)
+{
+    int rc = ensure_full(mu);
+    if (rc) return rc;
+    XmBatchArg a = {.in = in, .out = out, .batch = batch, .frames = out_frames, .place = place};
+    return run_all(mu, t_timeline, &a);
+}
+
+/* ---- streaming (host memory): every device streams its block ------------ */
+int xm_multi_stream_begin(XmMulti *mu, size_t batch)
+{
+    if (mu->cfg.mem_kind == XM_MEM_DEVICE) return XM_ENOSYS;
+    int rc = ensure_full(mu);
+    for (int d = 0; d < mu->n && !rc; ++d) {
+        block(batch, mu->n, d, &mu->st_first[d], &mu->st_cnt[d]);
+        if (mu->st_cnt[d]) rc = xm_audio_mixer_stream_begin(mu->sub[d], mu->st_cnt[d]);
+    }
+    mu->st_on = !rc;
+    return rc;
+}
+
+size_t xm_multi_stream_out_frames(const XmMulti *mu, size_t frames_in, int flush)
+{
+    if (!mu->st_on) return 0;
+    for (int d = 0; d < mu->n; ++d)   /* every active block releases the same frames */
+        if (mu->st_cnt[d]) return xm_audio_mixer_stream_out_frames(mu->sub[d], frames_in, flush);
+    return 0;
+}
+
+typedef struct {
+    const void *in;
+    void *out;
+    ptrdiff_t ts, ms, os;
+    size_t n, cap;
+    int flush;
+    size_t got[XM_MAX_DEVICES];
+} XmStreamArg;
+
+static int t_stream(XmMulti *mu, int d, void *p)
+{
+    XmStreamArg *a = p;
+    a->got[d] = 0;
+    if (!mu->st_cnt[d]) return XM_OK;
+    const char *in = a->in ? (const char *)a->in + (ptrdiff_t)mu->st_first[d] * a->ms * fmt_bytes(mu->cfg.sample_fmt)
+                           : NULL;
+    char *out = a->out ? (char *)a->out + (ptrdiff_t)mu->st_first[d] * a->os * out_elem(&mu->cfg) : NULL;
+    if (a->flush) return xm_audio_mixer_stream_flush(mu->sub[d], out, a->os, a->cap, &a->got[d]);
+    return xm_audio_mixer_stream_push(mu->sub[d], in, a->ts, a->ms, a->n, out, a->os, a->cap, &a->got[d]);
+}
+
+int xm_multi_stream_step(XmMulti *mu, const void *in, ptrdiff_t ts, ptrdiff_t ms, size_t n, void *out,
+                         ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush)
+{
+    if (frames_out) *frames_out = 0;
+    if (!mu->st_on || !frames_out) return XM_EINVAL;
+    if (mu->span_mode) return XM_EINVAL;   /* the track list changed mid-stream */
+    XmStreamArg a = {in, out, ts, ms, os, n, out_cap, flush, {0}};
+    int rc = run_all(mu, t_stream, &a);
+    for (int d = 0; d < mu->n; ++d)
+        if (mu->st_cnt[d]) {
+            *frames_out = a.got[d];
+            break;
+        }
+    if (flush || rc) mu->st_on = 0;
+    return rc;
+}
+
+/* ---- config 5: tracks spanning devices ----------------------------------- */
+typedef struct {
+    const void *const *in;
+    void *const *out;
+    ptrdiff_t ts, ms, os;
+    size_t batch, frames, fo, S, nb;
+    int phase;   /* 0 partials, 1 exchange by copies + finish, 2 finish after RCCL */
+} XmSpanArg;
+
+static int grow_on(int dev, void **p, size_t *cap, size_t need)
+{
+    if (*cap >= need) return XM_OK;
+    int rc = xmh_set_device(dev);
+    if (rc) return rc;
+    xmh_free(*p);
+    *p = NULL;
+    *cap = 0;
+    if ((rc = xmh_malloc(p, need))) return rc;
+    *cap = need;
+    return XM_OK;
+}
+
+static int t_span(XmMulti *mu, int d, void *p)
+{
+    const XmSpanArg *a = p;
+    XmAudioMixer *s = mu->sub[d];
+    const size_t blk = a->nb * a->S;   /* int32 per owned block */
+    int rc = xmh_set_device(mu->devs[d]);
+    if (rc) return rc;
+    if (a->phase == 0) {
+        rc = grow_on(mu->devs[d], &mu->part[d], &mu->part_cap[d], a->batch * a->S * sizeof(int32_t));
+        if (!rc) rc = xm_audio_mixer_process_partial_s16(s, a->in[d], a->ts, a->ms, (int32_t *)mu->part[d],
+                                                         (ptrdiff_t)a->S, a->batch, a->frames);
+        return rc;
+    }
+    if (a->phase == 1) {   /* block d of every device's partial, then the ordered sum over parts */
+        rc = grow_on(mu->devs[d], &mu->recv[d], &mu->recv_cap[d], (size_t)mu->n * blk * sizeof(int32_t));
+        void *st = xm_mixer_stream(s);
+        for (int q = 0; q < mu->n && !rc; ++q)
+            rc = xmh_memcpy_peer((int32_t *)mu->recv[d] + (size_t)q * blk, mu->devs[d],
+                                 (const int32_t *)mu->part[q] + (size_t)d * blk, mu->devs[q], blk * sizeof(int32_t),
+                                 st);
+        if (!rc)
+            rc = xm_audio_mixer_finish_s16(s, (const int32_t *)mu->recv[d], mu->n, (ptrdiff_t)blk, (ptrdiff_t)a->S,
+                                           (int16_t *)a->out[d], a->os, a->nb, a->fo);
+        return rc;
+    }
+    /* phase 2: the reduce-scatter already summed block d into recv[d] on this stream */
+    rc = xm_audio_mixer_finish_s16(s, (const int32_t *)mu->recv[d], 1, 0, (ptrdiff_t)a->S, (int16_t *)a->out[d],
+                                   a->os, a->nb, a->fo);
+    if (!rc) rc = xmh_comm_check(mu->comm[d]);
+    return rc;
+}
+
+int xm_multi_mix_spanning_s16(XmMulti *mu, const void *const *in, ptrdiff_t ts, ptrdiff_t ms, void *const *out,
+                              ptrdiff_t os, size_t batch, size_t frames_in)
+{
+    const int n = mu->n;
+    if (mu->cfg.sample_fmt != XM_FMT_S16 || mu->cfg.mem_kind != XM_MEM_DEVICE ||
+        (mu->cfg.flags & XM_MIXER_OUT_CONVERT))
+        return XM_ENOSYS;
+    if (!in || !out || mu->n_tracks % n || batch % (size_t)n) return XM_EINVAL;
+    for (int d = 0; d < n; ++d)
+        if (!in[d] || !out[d]) return XM_EINVAL;
+    if (batch == 0) return XM_OK;
+    const int per = mu->n_tracks / n;
+    if (!mu->span_mode) {   /* sub d holds its own tracks */
+        int rc = XM_OK;
+        for (int d = 0; d < n && !rc; ++d) rc = xm_audio_mixer_set_tracks(mu->sub[d], mu->tracks + d * per, per);
+        if (rc) {
+            set_full(mu);
+            return rc;
+        }
+        mu->span_mode = 1;
+    }
+    XmSpanArg a;
+    memset(&a, 0, sizeof a);
+    a.in = in;
+    a.out = out;
+    a.ts = ts;
+    a.ms = ms;
+    a.os = os;
+    a.batch = batch;
+    a.frames = frames_in;
+    a.fo = xm_resample_out_frames(mu->cfg.in_rate, mu->cfg.out_rate, frames_in);
+    a.S = a.fo * (size_t)mu->cfg.channels;
+    a.nb = batch / (size_t)n;
+    if (a.fo == 0) return XM_OK;
+    int rc = run_all(mu, t_span, &a);   /* 1) partials, joined */
+    if (rc) return rc;
+    if (!mu->distinct) {                /* 2) exchange by device copies + ordered finish */
+        a.phase = 1;
+        return run_all(mu, t_span, &a);
+    }
+    /* 2) one reduce-scatter over the devices (RCCL over xGMI), issued as one group */
+    if (!mu->comm_ready) {
+        if ((rc = xmh_comm_init_all(mu->comm, n, mu->devs))) return rc;
+        mu->comm_ready = 1;
+    }
+    for (int d = 0; d < n && !rc; ++d)
+        rc = grow_on(mu->devs[d], &mu->recv[d], &mu->recv_cap[d], a.nb * a.S * sizeof(int32_t));
+    if (rc) return rc;
+    if ((rc = xmh_group_start())) return rc;
+    for (int d = 0; d < n; ++d) {
+        int r2 = xmh_set_device(mu->devs[d]);
+        if (!r2)
+            r2 = xmh_reduce_scatter_i32((const int32_t *)mu->part[d], (int32_t *)mu->recv[d], a.nb * a.S, mu->comm[d],
+                                        xm_mixer_stream(mu->sub[d]));
+        if (!rc) rc = r2;
+    }
+    int r3 = xmh_group_end();
+    if (rc || r3) return rc ? rc : r3;
+    a.phase = 2;                        /* 3) saturate the owned blocks */
+    return run_all(mu, t_span, &a);
+}

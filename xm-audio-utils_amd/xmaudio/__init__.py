@@ -60,6 +60,8 @@ EXPORTED = [
     "xm_audio_mixer_stream_begin", "xm_audio_mixer_stream_out_frames", "xm_audio_mixer_stream_push",
     "xm_audio_mixer_stream_flush", "xm_effects_stream_reset", "xm_effects_process_stream",
     "xm_audio_mixer_process_timeline",
+    "xm_audio_mixer_create_multi", "xm_audio_mixer_n_devices", "xm_audio_mixer_process_sharded",
+    "xm_audio_mixer_mix_spanning_s16",
 ]
 
 
@@ -75,7 +77,7 @@ class XmTrackDesc(C.Structure):
 
 class XmMixerConfig(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("in_rate", "out_rate", "channels", "sample_fmt",
-                                          "mem_kind", "device", "flags", "reserved")]
+                                          "mem_kind", "device", "flags", "n_devices")]
 
 
 class XmMixerTiming(C.Structure):
@@ -133,6 +135,12 @@ _sigs = {
     "xm_audio_mixer_process_timeline": (_i, [_vp, C.POINTER(_vp), C.POINTER(XmTrackPlacement), C.POINTER(_vp),
                                              _sz, _sz]),
     "xm_effects_process_stream": (_i, [_vp, C.POINTER(_vp), C.POINTER(_vp), _sz, _sz]),
+    "xm_audio_mixer_create_multi": (_vp, [C.POINTER(XmMixerConfig), C.POINTER(_i), _i, C.POINTER(_i)]),
+    "xm_audio_mixer_n_devices": (_i, [_vp]),
+    "xm_audio_mixer_process_sharded": (_i, [_vp, C.POINTER(_vp), C.c_ssize_t, C.c_ssize_t, C.POINTER(_vp),
+                                            C.c_ssize_t, C.POINTER(_sz), _sz]),
+    "xm_audio_mixer_mix_spanning_s16": (_i, [_vp, C.POINTER(_vp), C.c_ssize_t, C.c_ssize_t, C.POINTER(_vp),
+                                             C.c_ssize_t, _sz, _sz]),
 }
 for _n, (_r, _a) in _sigs.items():
     if os.environ.get("XM_AUDIO_LIB") and not hasattr(_lib, _n):
@@ -209,11 +217,18 @@ class Mixer:
     """xm_audio_mixer_* handle."""
 
     def __init__(self, in_rate: int, out_rate: int, channels: int = 2, fmt: str = "f32",
-                 mem: str = "host", device: int = 0, convert_out: bool = False):
+                 mem: str = "host", device: int = 0, convert_out: bool = False, devices=None,
+                 n_devices: int = 0):
+        """devices: a device list -> multi-device handle (xm_audio_mixer_create_multi);
+        n_devices > 1: devices device .. device+n-1 (XmMixerConfig.n_devices)."""
         cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device,
-                            XM_MIXER_OUT_CONVERT if convert_out else 0, 0)
+                            XM_MIXER_OUT_CONVERT if convert_out else 0, n_devices)
         st = C.c_int(0)
-        self._h = _lib.xm_audio_mixer_create_ex(C.byref(cfg), C.byref(st))
+        if devices is not None:
+            dl = (C.c_int * len(devices))(*devices)
+            self._h = _lib.xm_audio_mixer_create_multi(C.byref(cfg), dl, len(devices), C.byref(st))
+        else:
+            self._h = _lib.xm_audio_mixer_create_ex(C.byref(cfg), C.byref(st))
         if not self._h:
             raise XmError(st.value, "xm_audio_mixer_create")
         self.cfg = cfg
@@ -338,6 +353,26 @@ class Mixer:
         _check(_lib.xm_audio_mixer_process_strided(self._h, in_ptr, in_track_stride, in_mix_stride, out_ptr,
                                                    out_mix_stride, batch, frames_in), "process_strided")
 
+
+    def n_devices(self) -> int:
+        return _lib.xm_audio_mixer_n_devices(self._h)
+
+    def process_sharded(self, in_ptrs, in_track_stride: int, in_mix_stride: int, out_ptrs,
+                        out_mix_stride: int, batches, frames_in: int):
+        """Multi-device, device memory resident per device: in_ptrs[d]/out_ptrs[d] on device d."""
+        n = len(in_ptrs)
+        _check(_lib.xm_audio_mixer_process_sharded(self._h, (C.c_void_p * n)(*in_ptrs), in_track_stride,
+                                                   in_mix_stride, (C.c_void_p * n)(*out_ptrs), out_mix_stride,
+                                                   (C.c_size_t * n)(*batches), frames_in), "process_sharded")
+
+    def mix_spanning_s16(self, in_ptrs, in_track_stride: int, in_mix_stride: int, out_ptrs,
+                         out_mix_stride: int, batch: int, frames_in: int):
+        """Config 5 in the library: device d holds tracks [d*T/n, (d+1)*T/n) of every mix at
+        in_ptrs[d] and receives the finished mixes [d*batch/n, (d+1)*batch/n) at out_ptrs[d]."""
+        n = len(in_ptrs)
+        _check(_lib.xm_audio_mixer_mix_spanning_s16(self._h, (C.c_void_p * n)(*in_ptrs), in_track_stride,
+                                                    in_mix_stride, (C.c_void_p * n)(*out_ptrs), out_mix_stride,
+                                                    batch, frames_in), "mix_spanning_s16")
 
     def process_partial_strided(self, in_ptr: int, in_track_stride: int, in_mix_stride: int, partial_ptr: int,
                                 partial_mix_stride: int, batch: int, frames_in: int):
