@@ -1,0 +1,198 @@
+"""TEST INFRASTRUCTURE ONLY — run by tests/test_host_asan.py in a child
+process with the ASan runtime preloaded and XM_AUDIO_LIB pointing at
+tests/host_asan/build/libxm_audio_asan.so (the host C layer over the CPU
+stand-in shim).  Drives every entry point of include/xm_audio_mixer.h and
+include/xm_effects.h through the same ctypes binding the GPU tests use, and
+compares the results with the C oracle bit for bit, so a sanitizer report
+or a wrong stride/pointer computation in src/*.c fails the run.  Prints
+"ALL HOST CHECKS PASSED" at the end."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for p in (os.path.join(ROOT, "xm-audio-utils_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+import xmaudio as xm  # noqa: E402
+import c_oracle as CO  # noqa: E402
+import np_oracle as O  # noqa: E402
+
+SEED = O.SEED
+RAMPS = [dict(gain0=0.9), dict(gain0=0.0, gain1=0.8, ramp_start=100, ramp_len=900),
+         dict(gain0=0.7, gain1=0.2, ramp_start=500, ramp_len=441), dict(gain0=0.5),
+         dict(mode=1, ramp_start=700, ramp_len=300), dict(gain0=0.0, gain1=1.0, ramp_start=700, ramp_len=300),
+         dict(gain0=1.25, gain1=0.75, ramp_start=0, ramp_len=1000), dict(gain0=0.3, gain1=0.6, ramp_start=800)]
+Q15 = [dict(gain0_q15=29491), dict(gain0_q15=0, gain1_q15=26214, ramp_start=0, ramp_len=480),
+       dict(gain0_q15=65535, gain1_q15=100, ramp_start=100, ramp_len=300), dict(gain0_q15=16384),
+       dict(mode=1, ramp_start=144, ramp_len=96), dict(gain0_q15=0, gain1_q15=32768, ramp_start=144, ramp_len=96),
+       dict(gain0_q15=40000, gain1_q15=3, ramp_start=400, ramp_len=13), dict(gain0_q15=7, gain1_q15=60000, ramp_start=480)]
+
+
+def check(name, ok):
+    print(("ok   " if ok else "FAIL ") + name, flush=True)
+    if not ok:
+        raise SystemExit(1)
+
+
+def beq(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def f32_tracks(B, ntr, N, C=2, base=0):
+    return np.stack([np.stack([O.gen_f32(SEED, base + 8 * b + t, C, N) for t in range(ntr)]) for b in range(B)])
+
+
+def s16_tracks(B, ntr, N, C=2, base=0):
+    return np.stack([np.stack([O.gen_s16(SEED, base + 8 * b + t, C, N) for t in range(ntr)]) for b in range(B)])
+
+
+def main():
+    # resample + mix, host memory, odd length, every gain form
+    x = f32_tracks(2, 8, 1201)
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(RAMPS)
+    y = m.process(x)
+    ref, _ = CO.batch_resample_mix_f32(x, RAMPS, 147, 160, threads=1)
+    check("f32 48k->44.1k 8-track mix (host memory)", beq(y, ref))
+    m.set_crossfade(0, 3, 200, 500)
+    y2 = m.process(x)
+    r2 = list(RAMPS)
+    r2[0] = dict(mode=1, ramp_start=200, ramp_len=500)
+    r2[3] = dict(gain0=0.0, gain1=1.0, ramp_start=200, ramp_len=500)
+    check("set_crossfade", beq(y2, CO.batch_resample_mix_f32(x, r2, 147, 160)[0]))
+
+    # config 1 shape (s16 mono 44.1k -> 48k), and the s16 Q15 mix
+    s = s16_tracks(1, 1, 4410, C=1)
+    r = xm.Mixer(44100, 48000, 1, "s16")
+    check("s16 44.1k->48k resample", beq(r.process(s)[0], CO.resample_s16(s[0, 0], 160, 147)))
+    q = s16_tracks(3, 8, 960)
+    mq = xm.Mixer(48000, 48000, 2, "s16")
+    mq.set_tracks(Q15)
+    check("s16 Q15 8-track mix", beq(mq.process(q), CO.batch_mix_s16(q, Q15)[0]))
+
+    # "device" memory: strided, irregular pointer tables, output conversion
+    d = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    d.set_tracks(RAMPS)
+    F = d.out_frames(1201)
+    yd = np.zeros((2, F, 2), np.float32)
+    d.process_strided(x.ctypes.data, 1201 * 2, 8 * 1201 * 2, yd.ctypes.data, F * 2, 2, 1201)
+    check("device-memory strided", beq(yd, ref))
+    xs = [np.ascontiguousarray(x[b, t]) for b in range(2) for t in range(8)]
+    outs = [np.zeros((F, 2), np.float32) for _ in range(2)]
+    d.process_ptrs([a.ctypes.data for a in xs], [o.ctypes.data for o in outs], 2, 1201)
+    check("device-memory irregular pointer tables", beq(np.stack(outs), ref))
+    c = xm.Mixer(48000, 44100, 2, "f32", convert_out=True)
+    c.set_tracks(RAMPS)
+    want = np.clip(np.rint(ref.astype(np.float32) * np.float32(32768)), -32768, 32767).astype(np.int16)
+    check("f32 mix -> s16 out", beq(c.process(x), want))
+
+    # config 5: partials and finish
+    p16 = s16_tracks(2, 16, 480)
+    ramps16 = Q15 + Q15
+    parts = np.zeros((2, 2, 480 * 2), np.int32)
+    for h in range(2):
+        ph = xm.Mixer(48000, 48000, 2, "s16", mem="device")
+        ph.set_tracks(ramps16[8 * h: 8 * h + 8])
+        xh = np.ascontiguousarray(p16[:, 8 * h: 8 * h + 8])
+        ph.process_partial_strided(xh.ctypes.data, 960, 8 * 960, parts[h].ctypes.data, 960, 2, 480)
+    yo = np.zeros((2, 480, 2), np.int16)
+    ph.finish_s16(parts.ctypes.data, 2, 2 * 960, 960, yo.ctypes.data, 960, 2, 480)
+    check("partial + finish_s16", beq(yo, CO.batch_mix_s16(p16, ramps16)[0]))
+
+    # streaming, ragged blocks (1-frame, empty, longer than the window)
+    m.set_tracks(RAMPS)
+    m.stream_begin(2)
+    outs, pos = [], 0
+    for n in (0, 1, 5, 300, 1, 0, 894):
+        outs.append(m.stream_push(x[:, :, pos:pos + n]))
+        pos += n
+    outs.append(m.stream_flush())
+    check("streaming resample+mix == whole signal", beq(np.concatenate(outs, axis=1), ref))
+
+    # timeline: per-track rates and placement
+    tl = xm.Mixer(44100, 48000, 1, "f32")
+    tl.set_tracks([dict(in_rate=22050, gain0=0.7), dict(in_rate=16000, gain0=0.4), dict(gain0=0.5)])
+    tr = [O.gen_f32(SEED, 900 + t, 1, 700 + 50 * t)[None] for t in range(3)]
+    yt = tl.process_timeline(tr, [0, 100, -30], 2000)
+    ys = []
+    for t, (rate, off) in enumerate(zip((22050, 16000, 44100), (0, 100, -30))):
+        from math import gcd
+        g = gcd(rate, 48000)
+        z = CO.resample_f32(tr[t][0], 48000 // g, rate // g)
+        pz = np.zeros((2000, 1), np.float32)
+        lo, hi = max(off, 0), min(off + len(z), 2000)
+        pz[lo:hi] = z[lo - off:hi - off]
+        ys.append(pz)
+    check("timeline mix", beq(yt[0], CO.mix_f32(ys, [dict(gain0=0.7), dict(gain0=0.4), dict(gain0=0.5)])))
+
+    # effects: biquad cascade + FIR, whole and streamed; per-track chain in the mixer
+    sos = np.array([O.rbj_section(0, 44100.0, 400.0, 3.0, 1.0), O.rbj_section(0, 44100.0, 3000.0, -2.0, 0.7)],
+                   np.float32)
+    h = np.linspace(-0.3, 0.5, 9).astype(np.float32)
+    e = xm.Effects(44100, 2)
+    for sv in sos:
+        e.add_biquad(sv)
+    e.add_fir(h)
+    xe = f32_tracks(3, 1, 777, base=50)[:, 0]
+    ye = e.process(xe)
+    re = np.stack([CO.fir_f32(CO.biquad_f32(xe[b], sos), h) for b in range(3)])
+    check("effects chain (biquad + FIR)", beq(ye, re))
+    e.stream_reset(3)
+    yst = np.concatenate([e.process_stream(xe[:, :1]), e.process_stream(xe[:, 1:1]), e.process_stream(xe[:, 1:400]),
+                          e.process_stream(xe[:, 400:])], axis=1)
+    check("effects streaming == whole", beq(yst, re))
+    mf = xm.Mixer(48000, 44100, 2, "f32")
+    mf.set_tracks(RAMPS)
+    mf.set_track_effects(e)
+    yf = mf.process(x)
+    rf = np.stack([CO.mix_f32([CO.fir_f32(CO.biquad_f32(CO.resample_f32(x[b, t], 147, 160), sos), h)
+                               for t in range(8)], RAMPS) for b in range(2)])
+    check("mixer with per-track effects", beq(yf, rf))
+
+    # multi-device handles (XM_FAKE_DEVICES=2): distinct devices and a repeated one
+    for devs in ([0, 1], [0, 0, 1]):
+        mm = xm.Mixer(48000, 44100, 2, "f32", devices=devs)
+        mm.set_tracks(RAMPS)
+        x5 = f32_tracks(5, 8, 601, base=200)
+        check(f"multi-device {devs} batch", beq(mm.process(x5), CO.batch_resample_mix_f32(x5, RAMPS, 147, 160)[0]))
+        mm.set_track_effects(e)
+        check(f"multi-device {devs} with effects",
+              beq(mm.process(x5), np.stack([CO.mix_f32([CO.fir_f32(CO.biquad_f32(CO.resample_f32(x5[b, t], 147, 160),
+                                                                                 sos), h) for t in range(8)], RAMPS)
+                                             for b in range(5)])))
+        mm.set_track_effects(None)
+        mm.stream_begin(5)
+        o1 = mm.stream_push(x5[:, :, :333])
+        o2 = mm.stream_push(x5[:, :, 333:])
+        o3 = mm.stream_flush()
+        check(f"multi-device {devs} streaming",
+              beq(np.concatenate([o1, o2, o3], axis=1), CO.batch_resample_mix_f32(x5, RAMPS, 147, 160)[0]))
+    q64 = s16_tracks(4, 64, 240, base=300)
+    ramps64 = (Q15 * 8)[:64]
+    want64 = CO.batch_mix_s16(q64, ramps64)[0]
+    for devs in ([0], [0, 1], [0, 0], [0, 1, 0, 1]):
+        n = len(devs)
+        sp = xm.Mixer(48000, 48000, 2, "s16", mem="device", devices=devs)
+        sp.set_tracks(ramps64)
+        per = 64 // n
+        ins = [np.ascontiguousarray(q64[:, d * per:(d + 1) * per]) for d in range(n)]
+        outs = [np.zeros((4 // n, 240, 2), np.int16) for _ in range(n)]
+        sp.mix_spanning_s16([a.ctypes.data for a in ins], 480, per * 480, [o.ctypes.data for o in outs], 480, 4, 240)
+        check(f"mix_spanning_s16 {devs}", beq(np.concatenate(outs), want64))
+
+    # argument errors never reach a kernel
+    bad = 0
+    for fn in (lambda: xm.Mixer(0, 48000), lambda: xm.Mixer(48000, 44100, 3),
+               lambda: m.set_tracks([dict(ramp_len=1 << 25)]), lambda: xm.Mixer(48000, 44100, devices=[0, 5])):
+        try:
+            fn()
+        except xm.XmError:
+            bad += 1
+    check("argument errors", bad == 4)
+    print("ALL HOST CHECKS PASSED", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -77,6 +77,58 @@ def vblock(ntaps, first, two):
     add(ntaps - 1)
     return "\\n\\t".join(lines)
 
+# SGPR pairs the literal-coefficient blocks load (clobbered by every block)
+LK_SGPR = (96, 98)
+
+
+def lblock(ntaps, first, two):
+    """Packed taps with literal coefficients (TAPS == 3): no scalar memory.
+    Per tap t the coefficient pair (h_k[t], h_k+1[t]) is written into an SGPR
+    pair by two s_mov_b32 (SALU, issued between the VALU of the previous tap;
+    the two pairs alternate by tap parity) and read by the two v_pk_mul_f32
+    exactly as the SGPR-pair operand of the TAPS == 2 blocks.  Operands: %0..%3
+    product temps (=&v), %4 a0, %5 a1 (accumulators), then per tap: h_k, h_k+1
+    ("i" bit patterns), x[ra+t], x[rb+t] (single-output blocks: h_k, x[ra+t])."""
+    lines = []
+    per = 4 if two else 2
+    def ops(t):
+        b = 6 + per * t
+        return (b, b + 1, b + 2, b + 3) if two else (b, None, b + 1, None)
+    def movs(t):
+        h0, h1, _, _ = ops(t)
+        sp = LK_SGPR[t % 2]
+        lines.append(f"s_mov_b32 s{sp}, %{h0}")
+        if two:
+            lines.append(f"s_mov_b32 s{sp + 1}, %{h1}")
+    def mul(t):
+        _, _, xa, xb = ops(t)
+        sp = LK_SGPR[t % 2]
+        tp = 2 * (t % 2)
+        if first and t == 0:
+            lines.append(f"v_pk_mul_f32 %4, s[{sp}:{sp + 1}], %{xa} op_sel_hi:[0,1]")
+            if two:
+                lines.append(f"v_pk_mul_f32 %5, s[{sp}:{sp + 1}], %{xb} op_sel:[1,0] op_sel_hi:[1,1]")
+            return
+        lines.append(f"v_pk_mul_f32 %{tp}, s[{sp}:{sp + 1}], %{xa} op_sel_hi:[0,1]")
+        if two:
+            lines.append(f"v_pk_mul_f32 %{tp + 1}, s[{sp}:{sp + 1}], %{xb} op_sel:[1,0] op_sel_hi:[1,1]")
+    def add(t):
+        if first and t == 0:
+            return
+        tp = 2 * (t % 2)
+        lines.append(f"v_pk_add_f32 %4, %4, %{tp}")
+        if two:
+            lines.append(f"v_pk_add_f32 %5, %5, %{tp + 1}")
+    movs(0)
+    mul(0)
+    for t in range(1, ntaps):
+        movs(t)
+        mul(t)
+        add(t - 1)
+    add(ntaps - 1)
+    return "\\n\\t".join(lines)
+
+
 out = ["// generated by tools/gen_pk_asm.py; do not edit", "#pragma once"]
 for n in range(1, 5):
     for first in (True, False):
@@ -85,5 +137,12 @@ for n in range(1, 5):
 for first, n, name in ((True, 8, "G0"), (False, 8, "G1"), (False, 6, "G2")):
     for two in (True, False):
         out.append(f'#define XM_PK_{name}_{"TWO" if two else "ONE"} "{block(n, first, two)}"')
+for n in (2, 4):
+    for first in (True, False):
+        for two in (True, False):
+            if first and n == 2:
+                continue
+            out.append(f'#define XM_LK_{"F" if first else "R"}{n}_{"TWO" if two else "ONE"} "{lblock(n, first, two)}"')
+out.append(f'#define XM_LK_CLOBBER "s{LK_SGPR[0]}", "s{LK_SGPR[0] + 1}", "s{LK_SGPR[1]}", "s{LK_SGPR[1] + 1}"')
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "xm_pk_taps.h")
 open(path, "w").write("\n".join(out) + "\n")

@@ -23,10 +23,11 @@ import numpy as np
 # load itself ("No HIP GPUs are available").  So when torch is installed,
 # load it first: libxm_audio.so then binds to torch's runtime and both share
 # one HIP context (device memory, streams) in the same process.
-try:  # pragma: no cover - environment dependent
-    import torch  # noqa: F401
-except ImportError:
-    pass
+if not os.environ.get("XM_NO_TORCH"):   # XM_NO_TORCH: the host-only sanitizer build (tests/host_asan)
+    try:  # pragma: no cover - environment dependent
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # XM_AUDIO_LIB: load another build of the same library (dev: ablation builds)
