@@ -315,14 +315,19 @@ def test_errors(xm, gpu):
 def test_biquad_cascade_shapes(xm, gpu, n_sos, channels):
     """Section-pipelined biquad kernel (lane = clip x section): every cascade
     length up to XM_MAX_SOS, more clips than one wave holds, ragged lengths
-    around the 32-frame chunk, bit-compared with the C oracle (sosfilt order)."""
+    around the 64-granule chunk (128 stereo / 256 mono frames: whole chunks,
+    a partial last chunk, one frame past a chunk), bit-compared with the C
+    oracle (sosfilt order)."""
     z = golden("effects.npz")
     rng = np.random.default_rng(n_sos * 10 + channels)
     sos = np.concatenate([z["sos"]] * 3)[:n_sos]
     e = xm.Effects(48000, channels)
     for s in sos:
         e.add_biquad(s)
-    for B, N in [(1, 1), (3, 31), (2 * (64 // n_sos) + 1, 33), (17, 1000)]:
+    ch = 256 // channels
+    kpw = min(64 // n_sos, 16)
+    for B, N in [(1, 1), (3, 31), (2 * kpw + 1, 33), (17, 1000), (5, ch), (kpw, 2 * ch), (3, 3 * ch + 1),
+                 (kpw + 1, 4 * ch - 1)]:
         x = (rng.standard_normal((B, N, channels)) * 0.5).astype(np.float32)
         y = e.process(x)
         for b in range(B):
@@ -395,3 +400,42 @@ def test_partial_errors(xm, gpu):
     with pytest.raises(xm.XmError) as e:
         h.finish_s16(1, 1, 0, 2, 1, 2, 1, 1)
     assert e.value.code == xm.XM_ENOSYS
+
+
+def test_biquad_pointer_tables_unaligned_and_far_apart(xm, gpu):
+    """The biquad kernel's two addressing forms: clips within 4 GB of the
+    wave's lowest one (wave-uniform base + 32-bit offsets) and clips further
+    apart (per-access 64-bit bases), with float-aligned (not 16-B aligned)
+    clip starts, out of place and in place."""
+    import torch
+    z = golden("effects.npz")
+    sos = np.concatenate([z["sos"]] * 2)[:5]
+    e = xm.Effects(48000, 2, mem="device")
+    for s in sos:
+        e.add_biquad(s)
+    N, B = 1000, 5
+    rng = np.random.default_rng(77)
+    x = (rng.standard_normal((B, N, 2)) * 0.5).astype(np.float32)
+    want = [CO.biquad_f32(x[b], sos) for b in range(B)]
+    big = torch.zeros(((5 << 30) // 4,), dtype=torch.float32, device="cuda")   # 5 GiB
+    small = torch.zeros((2 * N + 8,), dtype=torch.float32, device="cuda")
+    dst = torch.zeros((B * (N * 2 + 8),), dtype=torch.float32, device="cuda")
+    # clip starts: odd float offsets; clips 1 and 3 more than 4 GB above clip 0
+    offs = [1, (4 << 30) // 4 + 3, 4 * N + 5, (4 << 30) // 4 + 2 * N + 11]
+    views = [big[o:o + 2 * N] for o in offs] + [small[3:3 + 2 * N]]
+    for b, v in enumerate(views):
+        v.copy_(torch.from_numpy(x[b].reshape(-1)))
+    outs = [dst[(b + 1) * (2 * N + 8) - 2 * N - 1:(b + 1) * (2 * N + 8) - 1] for b in range(B - 1)]
+    outs.append(big[7 * N + 1:9 * N + 1])
+    torch.cuda.synchronize()
+    e.process_ptrs([v.data_ptr() for v in views], [o.data_ptr() for o in outs], N)
+    torch.cuda.synchronize()
+    for b in range(B):
+        assert bits_equal(outs[b].cpu().numpy().reshape(N, 2), want[b]), b
+    # in place, the same far-apart table
+    e.process_ptrs([v.data_ptr() for v in views], [v.data_ptr() for v in views], N)
+    torch.cuda.synchronize()
+    for b in range(B):
+        assert bits_equal(views[b].cpu().numpy().reshape(N, 2), want[b]), b
+    del big, small, dst
+    torch.cuda.empty_cache()

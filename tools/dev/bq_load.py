@@ -1,5 +1,5 @@
 """Dev: config-4 biquad stage alone (1024 stereo clips x 441000 frames, 5-band
-EQ, device memory, in place), for PMC passes on k_biquad_lanes."""
+EQ, device memory, in place), for timing and PMC passes on k_biquad_pipe."""
 import sys
 import time
 sys.path[:0] = ["xm-audio-utils_amd", "oracle"]
@@ -19,3 +19,14 @@ for it in range(2):
     e.process_ptrs(ptrs, ptrs, N)
     torch.cuda.synchronize()
     print(f"biquad pass {it}: {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+# dev builds with -DXM_BQ_PROF: per-wave cycle split of the last pass
+import ctypes
+import numpy as np
+fn = getattr(xm._lib, "xmh_dev_bq_prof", None)
+if fn is not None:
+    buf = np.zeros(4096, np.uint64)
+    fn(buf.ctypes.data_as(ctypes.c_void_p))
+    w = buf.reshape(2048, 2)[:(B + 11) // 12].astype(np.float64)
+    steps = (N + 127) // 128 + 4
+    print("compute wave, cycles per 128-frame step: chunk %.0f  barrier/wait %.0f" % tuple(w.mean(0) / steps),
+          flush=True)

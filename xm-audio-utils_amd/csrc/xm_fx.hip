@@ -4,30 +4,56 @@
 // Biquad: scipy sosfilt order (transposed DF-II, _signaltools.py:4601),
 // sections in order, state zero at clip start.  The recurrence is serial in
 // time, so exactness (SURVEY.md §7 hard part 3) limits the parallelism to
-// clips x sections: k_biquad_lanes gives each (clip, section) its own lane
-// and chains the sections through LDS chunks (see the comment at the kernel).
+// clips x sections: k_biquad_pipe gives each (clip, section) its own lane
+// and chains the sections through LDS (see the comment at the kernel).
 // FIR: upfirdn order (_upfirdn.py:107), taps staged in LDS, input tile in LDS.
 #include <stdlib.h>
+#include <algorithm>
+#include <atomic>
 #include "xm_device.h"
+
+// The LDS-DMA asm blocks set M0 themselves and list it as clobbered; clang
+// warns because M0 is reserved.  Nothing else in these kernels uses M0 (no
+// indirect register indexing, no ds_*_addtid / GWS: checked in the ISA).
+#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace {
 
-constexpr int BQ_MAXSEC = 15;   // XM_MAX_SOS (src/xm_internal.h): >= 4 clips per wave
+constexpr int BQ_MAXSEC = 15;   // XM_MAX_SOS (src/xm_internal.h): >= 4 clips per workgroup
 
 // Section-pipelined cascade.  The recurrence of one section is serial in
 // time, so the only parallelism that keeps sosfilt's rounding is across
 // clips and across sections: lane = (clip k, section s), lane = k*NS + s,
-// 64 / NS clips per wave (stereo (L, R) ride in one packed v_pk_* pair).
-// Time advances in chunks of CH frames; at step i lane s filters chunk i - s,
-// so the NS sections of a clip work on NS consecutive chunks at once and the
-// per-sample recurrence (4 dependent ops) is the only serial chain.
-//   section 0   reads its clip from HBM two chunks ahead into registers and
-//               passes the chunk through LDS like every other section;
-//   section s   reads the chunk lane - 1 (section s - 1) wrote one step earlier;
-//   last        stores to global memory instead of LDS.
-// One wave, so LDS needs no barrier: every read of a step precedes, in
-// program order, every write of that step.
-// In LDS a chunk is [CH / FPL][64 lanes][FPL frames] (16 B per lane-granule).
+// KPW = min(64 / NS, 16) clips per workgroup (stereo (L, R) ride in one
+// packed v_pk_* pair).  Time advances in chunks of BQ_G = 64 granules (16 B
+// each: FPL = 4 / C frames); at step i lane s filters chunk i - s, so the NS
+// sections of a clip work on NS consecutive chunks at once and the
+// per-sample recurrence is the only serial chain.
+//
+// Two waves per workgroup.  The compute wave runs only the recurrences:
+// section 0 reads granule g of its input at inb[i & 1][k][g], section s > 0
+// at sec[L - 1][g] (the previous section's output row), the last section
+// writes outb[i & 1][k][g], the others sec[L][g].  A lane reads granule g
+// (two granules ahead of its use) before its left neighbour overwrites it
+// with the next chunk: one wave, program order.  The copy wave does every
+// HBM access: per step, chunk i + 1 of each clip by one LDS-DMA instruction
+// (global_load_lds_dwordx4: 64 lanes x 16 B = the clip's whole 1 KB chunk,
+// a wave-uniform base, landing straight in its inb row) and the stores of
+// the chunk the last sections finished one step earlier (outb[(i - 1) & 1]);
+// it waits for its DMA and meets the compute wave at one s_barrier per step.
+// Rows are padded by one granule, so a wave's 64 row accesses of one granule
+// are bank-conflict free.  The DMA is issued from inline asm (the compiler
+// would otherwise put a vmcnt(0) before every LDS read); a partial last
+// chunk is loaded and stored element by element, with bounds.
+//
+// Measured on MI355X, config-4 biquad stage (1024 stereo clips x 441000
+// frames x 5 sections, tools/dev/bq_load.py): 22.3 ms for the previous
+// design (32-granule chunks, per-item exec-masked loads, register staging,
+// scattered 16-B items); 16.0 ms with one wave doing both jobs; 14.1 ms with
+// the copy wave.  The compute wave spends ~58 cycles per frame (9 packed
+// VALU ops + 1 LDS access per frame; tools/ubench/bq_chain.hip: ~51 cycles
+// for the bare recurrence with its LDS traffic), against a floor of
+// 36 cycles for 9 wave64 VALU issues.
 template <int C>
 struct BqVec;
 template <>
@@ -35,76 +61,250 @@ struct BqVec<1> { typedef float T; };
 template <>
 struct BqVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
 typedef float bq_f4 __attribute__((ext_vector_type(4)));
+typedef float bq_f2 __attribute__((ext_vector_type(2)));
+// 4-B aligned 16-B vector: clip bases are only float-aligned
+typedef float bq_f4u __attribute__((ext_vector_type(4), aligned(4)));
 
-template <int C, int CH, bool ST>
-__global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
+// One stereo granule (two frames A, B) of one section, hand-scheduled: the
+// per-frame chain z0 -> o -> a1*o -> u -> z0 is four dependent packed ops,
+// and every one of them has an independent op between it and its producer,
+// so a lone wave never stalls on the VALU forwarding latency and needs no
+// s_nop (the compiler's order put each product right before its consumer).
+// Same operations as the scalar form in k_biquad_pipe, bit for bit:
+// o = b0*v + z0, z0 = (b1*v - a1*o) + z1, z1 = b2*v - a2*o, with -(a*o) as a
+// negated product and the adds commuted (IEEE add is commutative).
+__device__ __forceinline__ bq_f4 bq_step2(bq_f4 v4, bq_f2 &z0, bq_f2 &z1, bq_f2 b0, bq_f2 b1, bq_f2 b2,
+                                          bq_f2 a1, bq_f2 a2)
+{
+    const bq_f2 va = {v4[0], v4[1]}, vb = {v4[2], v4[3]};
+    bq_f2 oa, ob, p0, p1, p2, t, u;
+    asm volatile(
+        "v_pk_mul_f32 %[p0], %[b0], %[va]\n\t"
+        "v_pk_mul_f32 %[p1], %[b1], %[va]\n\t"
+        "v_pk_add_f32 %[oa], %[z0], %[p0]\n\t"
+        "v_pk_mul_f32 %[p2], %[b2], %[va]\n\t"
+        "v_pk_mul_f32 %[t], %[a1], %[oa] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[p0], %[b0], %[vb]\n\t"
+        "v_pk_add_f32 %[t], %[p1], %[t]\n\t"
+        "v_pk_mul_f32 %[u], %[a2], %[oa] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[z0], %[z1], %[t]\n\t"
+        "v_pk_add_f32 %[z1], %[p2], %[u]\n\t"
+        "v_pk_add_f32 %[ob], %[z0], %[p0]\n\t"
+        "v_pk_mul_f32 %[p1], %[b1], %[vb]\n\t"
+        "v_pk_mul_f32 %[t], %[a1], %[ob] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[p2], %[b2], %[vb]\n\t"
+        "v_pk_add_f32 %[t], %[p1], %[t]\n\t"
+        "v_pk_mul_f32 %[u], %[a2], %[ob] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[z0], %[z1], %[t]\n\t"
+        "v_pk_add_f32 %[z1], %[p2], %[u]"
+        : [oa] "=&v"(oa), [ob] "=&v"(ob), [p0] "=&v"(p0), [p1] "=&v"(p1), [p2] "=&v"(p2), [t] "=&v"(t),
+          [u] "=&v"(u), [z0] "+v"(z0), [z1] "+v"(z1)
+        : [va] "v"(va), [vb] "v"(vb), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [a1] "v"(a1), [a2] "v"(a2));
+    return bq_f4{oa.x, oa.y, ob.x, ob.y};
+}
+
+constexpr int BQ_G = 64;     // granules per chunk = lanes per DMA instruction
+constexpr int BQ_KPW = 16;   // clips per wave at most (16 DMA + 16 stores per step)
+constexpr size_t BQ_LDS = (size_t)(64 + 4 * BQ_KPW) * (BQ_G + 1) * 16;   // 133,120 B
+
+#ifdef XM_BQ_PROF
+__device__ uint64_t g_bq_prof[4096];   // dev: per-workgroup cycles (compute wave: chunk, barrier wait)
+#endif
+
+template <int C, bool ST>
+__global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
 {
     typedef typename BqVec<C>::T V;
-    typedef const __attribute__((address_space(1))) bq_f4 gcf4;
-    typedef __attribute__((address_space(1))) bq_f4 gf4;
+    typedef const __attribute__((address_space(1))) float gcf;
+    typedef __attribute__((address_space(1))) float gf;
+    typedef __attribute__((address_space(1))) bq_f4u gf4u;
+    typedef __attribute__((address_space(3))) void lds_void;
+    constexpr int G = BQ_G;
     constexpr int FPL = 4 / C;                     // frames per 16-B granule
-    constexpr int G = CH / FPL;                    // granules per chunk
-    __shared__ bq_f4 in_buf[G][64];                // section 0's input
-    __shared__ bq_f4 sec_buf[G][64];               // output of lane's section (s < NS - 1)
+    constexpr int CH = G * FPL;                    // frames per chunk
+    constexpr uint32_t ROWB = (G + 1) * 16, PARB = BQ_KPW * ROWB;
+    // dynamic LDS (BQ_LDS bytes), rows padded by one granule:
+    //   inb[parity][clip][granule]   input chunks (DMA targets, below 64 KB)
+    //   outb[parity][clip][granule]  the last sections' output chunks
+    //   sec[lane][granule]           the other sections' output chunks
+    extern __shared__ bq_f4 bq_lds[];
+    bq_f4 (*inb)[BQ_KPW][G + 1] = (bq_f4 (*)[BQ_KPW][G + 1])bq_lds;
+    bq_f4 (*outb)[BQ_KPW][G + 1] = (bq_f4 (*)[BQ_KPW][G + 1])(bq_lds + 2 * BQ_KPW * (G + 1));
+    bq_f4 (*sec)[G + 1] = (bq_f4 (*)[G + 1])(bq_lds + 4 * BQ_KPW * (G + 1));
     const int ns = j.n_sos;
-    const int kpw = 64 / ns;                       // clips per wave
-    const int lane = threadIdx.x;
-    const int s = lane % ns, kk = lane / ns;
-    const int clip = blockIdx.x * kpw + kk;
-    const bool valid = kk < kpw && clip < j.n_clips;
-    const bool first = s == 0, last = s == ns - 1;
+    const int kpw = min(64 / ns, BQ_KPW);          // clips per workgroup
+    const int lane = threadIdx.x & 63;
+    const int clip0 = blockIdx.x * kpw;
+    const int nclip = min(kpw, j.n_clips - clip0);
     const int64_t N = j.frames;
     const int64_t nchunk = (N + CH - 1) / CH;
-    const float *x = valid ? j.in_ptrs[clip] : nullptr;
-    float *y = valid ? j.out_ptrs[clip] : nullptr;
-    const bq_f4 *src = first ? &in_buf[0][lane] : &sec_buf[0][(lane + 63) & 63];
+    const int64_t nfull = N / CH;                  // chunks with no frame past N
+    const int64_t steps = nchunk + ns - 1;
 
-    const float *q = j.sos + 6 * s;                 // this lane's section, state zero at clip start
+    if (threadIdx.x >= 64) {
+        // ---------------- copy wave: every HBM access of the workgroup ----------
+        // The clip bases.  Lane k < nclip holds clip k's pointers; when the
+        // clips lie within 4 GB of the lowest one (one tensor, or any compact
+        // table) every access is a wave-uniform base (SGPR: the lowest pointer
+        // + the chunk offset) plus a 32-bit per-lane offset precomputed per
+        // clip.  Otherwise each access broadcasts its clip's 64-bit pointer.
+        const int kl = min(lane, nclip - 1);
+        const uint64_t xl = (uint64_t)(uintptr_t)j.in_ptrs[clip0 + kl];
+        const uint64_t yl = (uint64_t)(uintptr_t)j.out_ptrs[clip0 + kl];
+        auto bcast = [&](uint64_t v, int k) __attribute__((always_inline)) {
+            // (readlane returns int: cast through uint32_t, no sign extension)
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), k) << 32) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, k);
+        };
+        uint64_t xmin = bcast(xl, 0), xmax = xmin, ymin = bcast(yl, 0), ymax = ymin;
+#pragma unroll
+        for (int k = 1; k < BQ_KPW; ++k) {
+            const uint64_t xk = bcast(xl, k), yk = bcast(yl, k);
+            xmin = xk < xmin ? xk : xmin; xmax = xk > xmax ? xk : xmax;
+            ymin = yk < ymin ? yk : ymin; ymax = yk > ymax ? yk : ymax;
+        }
+        const bool narrow = xmax - xmin < (1ull << 32) - 1024 && ymax - ymin < (1ull << 32) - 1024;
+        uint32_t dx[BQ_KPW], dy[BQ_KPW];          // per clip: offset from the base + this lane's granule
+#pragma unroll
+        for (int k = 0; k < BQ_KPW; ++k) {
+            dx[k] = (uint32_t)(bcast(xl, k) - xmin) + (uint32_t)lane * 16u;
+            dy[k] = (uint32_t)(bcast(yl, k) - ymin) + (uint32_t)lane * 16u;
+        }
+        const uint32_t loff = (uint32_t)lane * 16u;
+        const uint32_t inb0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)&inb[0][0][0]);
+
+        // input chunk c of every clip -> inb[c & 1]: one LDS-DMA instruction per
+        // clip (64 lanes x 16 B = the clip's whole chunk, straight into its row)
+        auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
+            if (c >= nchunk) return;
+            const uint32_t dst = inb0 + (uint32_t)(c & 1) * PARB;
+            if (c < nfull) {
+                const uint64_t cbb = (uint64_t)c * CH * C * 4;
+                if (narrow) {
+#pragma unroll
+                    for (int k = 0; k < BQ_KPW; ++k) {
+                        if (k >= nclip) break;     // wave-uniform
+                        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                                     :
+                                     : "s"(dst + (uint32_t)k * ROWB), "v"(dx[k]), "s"(xmin + cbb)
+                                     : "memory", "m0");
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < BQ_KPW; ++k) {
+                        if (k >= nclip) break;
+                        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                                     :
+                                     : "s"(dst + (uint32_t)k * ROWB), "v"(loff), "s"(bcast(xl, k) + cbb)
+                                     : "memory", "m0");
+                    }
+                }
+                return;
+            }
+            // partial last chunk: element loads with bounds, zero past N
+            const int64_t f0 = c * CH + lane * FPL;
+#pragma unroll
+            for (int k = 0; k < BQ_KPW; ++k) {
+                if (k >= nclip) break;
+                const float *x = (const float *)(uintptr_t)bcast(xl, k) + (size_t)f0 * C;
+                bq_f4 v = bq_f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (f0 * C + e < N * C) v[e] = ((gcf *)x)[e];
+                inb[c & 1][k][lane] = v;
+            }
+        };
+        // the last sections' chunk c (in outb[p]) -> HBM
+        auto store_chunk = [&](int64_t c, int p) __attribute__((always_inline)) {
+            if (c < 0 || c >= nchunk) return;
+            bq_f4 sv[BQ_KPW];
+#pragma unroll
+            for (int k = 0; k < BQ_KPW; ++k) sv[k] = outb[p][min(k, nclip - 1)][lane];
+            if (c < nfull) {
+                const uint64_t cbb = (uint64_t)c * CH * C * 4;
+#pragma unroll
+                for (int k = 0; k < BQ_KPW; ++k) {
+                    if (k >= nclip) break;
+                    if (narrow) *(gf4u *)((char *)(uintptr_t)(ymin + cbb) + dy[k]) = sv[k];
+                    else *(gf4u *)((char *)(uintptr_t)(bcast(yl, k) + cbb) + loff) = sv[k];
+                }
+                return;
+            }
+            const int64_t f0 = c * CH + lane * FPL;
+#pragma unroll
+            for (int k = 0; k < BQ_KPW; ++k) {
+                if (k >= nclip) break;
+                float *y = (float *)(uintptr_t)bcast(yl, k) + (size_t)f0 * C;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (f0 * C + e < N * C) ((gf *)y)[e] = sv[k][e];
+            }
+        };
+
+        load_chunk(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int64_t i = 0; i < steps; ++i) {
+            // the compute wave filters step i meanwhile
+            load_chunk(i + 1);
+            store_chunk(i - ns, (int)((i - 1) & 1));   // finished in step i - 1
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk i + 1 landed
+            __syncthreads();
+        }
+        store_chunk(steps - ns, (int)((steps - 1) & 1));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the LDS is gone
+        return;
+    }
+
+    // ---------------- compute wave: the recurrences -------------------------
+    const int s = lane % ns, kk = lane / ns;
+    const bool valid = kk < nclip;
+    const float *q = j.sos + 6 * s;                // this lane's section, state zero at clip start
     const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
+    const bq_f2 cb0 = {b0, b0}, cb1 = {b1, b1}, cb2 = {b2, b2}, ca1 = {a1, a1}, ca2 = {a2, a2};
     V z0 = V(0.0f), z1 = V(0.0f);
-    float *st = (ST && valid) ? j.state + ((size_t)clip * ns + s) * 2 * C : nullptr;
+    float *st = (ST && valid) ? j.state + ((size_t)(clip0 + kk) * ns + s) * 2 * C : nullptr;
     if (ST && st) {                                // streaming: continue from the previous block
         if constexpr (C == 2) { z0 = V{st[0], st[1]}; z1 = V{st[2], st[3]}; }
         else { z0 = st[0]; z1 = st[1]; }
     }
-
-    bq_f4 pa[G], pb[G];                            // section 0: chunks i and i + 1 in flight
-    auto load = [&](bq_f4 (&d)[G], int64_t c) {
-        if (!(first && valid && c < nchunk) || (j.dev_flags & 1)) return;   // dev_flags 1: attribution, no loads
-        const float *xc = x + (size_t)C * (size_t)(c * CH);
-        if ((c + 1) * CH <= N && (((uintptr_t)xc) & 15) == 0) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) d[g] = ((gcf4 *)xc)[g];
-        } else {
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    d[g][e] = (c * CH + g * FPL) * C + e < N * C ? xc[g * 4 + e] : 0.0f;
-        }
-    };
-    auto step = [&](int64_t i, bq_f4 (&cur)[G]) {
-        if (first) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) in_buf[g][lane] = cur[g];
-        }
-        load(cur, i + 2);                          // refill: chunk i + 2
+    const int kc = min(kk, BQ_KPW - 1);
+    const bq_f4 *srow = &sec[(lane + 63) & 63][0];
+    const bool last = s == ns - 1 && valid;        // idle lanes write their own (unread) sec row
+#ifdef XM_BQ_PROF
+    uint64_t pr[2] = {0, 0}, tq = __builtin_amdgcn_s_memtime();
+#define XM_BQ_T(n) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pr[n] += t_ - tq; tq = t_; } while (0)
+#else
+#define XM_BQ_T(n) do { } while (0)
+#endif
+    __syncthreads();
+    for (int64_t i = 0; i < steps; ++i) {
+        XM_BQ_T(1);
         const int64_t c = i - s;                   // chunk this lane filters
-        bq_f4 v4[G];
+        // every lane runs the chunk (uniform control flow); a lane outside its
+        // chunk range keeps its state and its outputs are never stored
+        const bool act = valid && c >= 0 && c < nchunk;
+        const V z0s = z0, z1s = z1;
+        // the last chunk's frames past N are zero padding: with a state to
+        // carry they must not advance the recurrence
+        const bool tail = ST && st && act && (c + 1) * CH > N;
+        const bq_f4 *src = s ? srow : &inb[i & 1][kc][0];
+        bq_f4 *dst = last ? &outb[i & 1][kc][0] : &sec[lane][0];
+        // fully unrolled over the chunk: granule g + 2 is read while granule
+        // g is filtered, so the LDS latency hides behind two granules
+        bq_f4 n0 = src[0], n1 = src[1];
 #pragma unroll
-        for (int g = 0; g < G; ++g) v4[g] = src[g * 64];
-        if (c >= 0 && c < nchunk) {
-            // the last chunk's frames past N are zero padding: with a state
-            // to carry they must not advance the recurrence
-            const bool tail = ST && st && (c + 1) * CH > N;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
+        for (int g = 0; g < G; ++g) {
+            const bq_f4 v4 = n0;
+            n0 = n1;
+            if (g + 2 < G) n1 = src[g + 2];
+            auto scalar = [&]() __attribute__((always_inline)) {
                 bq_f4 r;
 #pragma unroll
                 for (int e = 0; e < FPL; ++e) {
                     V v;
-                    if constexpr (C == 2) v = V{v4[g][2 * e], v4[g][2 * e + 1]};
-                    else v = v4[g][e];
+                    if constexpr (C == 2) v = V{v4[2 * e], v4[2 * e + 1]};
+                    else v = v4[e];
                     const V o = b0 * v + z0;              // sosfilt (_sosfilt.pyx) order
                     if (tail && c * CH + g * FPL + e >= N) {
                         // padding frame: output unused, state kept
@@ -115,159 +315,26 @@ __global__ __launch_bounds__(64) void k_biquad_lanes(XmhFxJob j)
                     if constexpr (C == 2) { r[2 * e] = o.x; r[2 * e + 1] = o.y; }
                     else r[e] = o;
                 }
-                v4[g] = r;
-            }
-            if (!last) {
-#pragma unroll
-                for (int g = 0; g < G; ++g) sec_buf[g][lane] = v4[g];
-            } else if (valid) {
-                float *yc = y + (size_t)C * (size_t)(c * CH);
-                if ((c + 1) * CH <= N && (((uintptr_t)yc) & 15) == 0) {
-#pragma unroll
-                    for (int g = 0; g < G; ++g) ((gf4 *)yc)[g] = v4[g];
-                } else {
-#pragma unroll
-                    for (int g = 0; g < G; ++g)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if ((c * CH + g * FPL) * C + e < N * C) yc[g * 4 + e] = v4[g][e];
-                }
-            }
+                return r;
+            };
+            bq_f4 r;
+            if constexpr (C == 2) r = tail ? scalar() : bq_step2(v4, z0, z1, cb0, cb1, cb2, ca1, ca2);
+            else r = scalar();
+            dst[g] = r;
         }
-    };
-    load(pa, 0);
-    load(pb, 1);
-    const int64_t steps = nchunk + ns - 1;
-    // Lane s reads, at step i, what lane s - 1 wrote at step i - 1: a
-    // cross-lane hand-off through LDS.  The wave barrier between steps orders
-    // every LDS access of step i before every one of step i + 1 for the
-    // compiler as well (free in a one-wave workgroup).
-    for (int64_t i = 0; i < steps; i += 2) {
-        step(i, pa);
-        __builtin_amdgcn_wave_barrier();
-        if (i + 1 < steps) step(i + 1, pb);
-        __builtin_amdgcn_wave_barrier();
+        if (!act) { z0 = z0s; z1 = z1s; }
+        XM_BQ_T(0);
+        __syncthreads();                           // chunk i + 1 staged; outputs visible to the copy wave
     }
+#ifdef XM_BQ_PROF
+    if (lane == 0 && blockIdx.x < 2048)
+        for (int n = 0; n < 2; ++n) g_bq_prof[blockIdx.x * 2 + n] = pr[n];
+#endif
+#undef XM_BQ_T
     if (ST && st) {
         if constexpr (C == 2) { st[0] = z0.x; st[1] = z0.y; st[2] = z1.x; st[3] = z1.y; }
         else { st[0] = z0; st[1] = z1; }
     }
-}
-
-// Stereo cascade with one channel per lane: lane = (clip k, channel ch,
-// section s) = (k*2 + ch)*NS + s, 64 / (2*NS) clips per wave.  Same chunked
-// section pipeline as k_biquad_lanes, but the recurrence runs on plain fp32
-// ops: a wave64 v_pk_*_f32 issues in ~4.3 clk per SIMD against ~2.4 clk for
-// v_mul/v_add_f32 (tools/ubench/valu_rate.hip), and a lane's per-frame
-// instruction stream (9 ops around a 4-op dependent chain) was expected to
-// bound the time.  Measured on config 4 it is slower (EQ 23.3 ms against 20.3
-// for packed lanes), so it is kept for A/B only
-// (XM_BQ_SPLIT=1); the product uses k_biquad_lanes.  Arithmetic per channel is
-// sosfilt's, unchanged.  Section 0 loads whole interleaved granules (both
-// channel lanes read the same 32 B) and keeps its channel; the last section
-// stores its channel's samples (the two channel lanes fill each 8-B frame).
-template <int CH, bool ST>
-__global__ __launch_bounds__(64) void k_biquad_split(XmhFxJob j)
-{
-    typedef const __attribute__((address_space(1))) bq_f4 gcf4;
-    constexpr int G = CH / 4;                      // mono granules (4 frames) per chunk
-    __shared__ bq_f4 in_buf[G][64];
-    __shared__ bq_f4 sec_buf[G][64];
-    const int ns = j.n_sos;
-    const int lpc = 2 * ns;                        // lanes per clip
-    const int kpw = 64 / lpc;
-    const int lane = threadIdx.x;
-    const int s = lane % ns, ch = (lane / ns) & 1, kk = lane / lpc;
-    const int clip = blockIdx.x * kpw + kk;
-    const bool valid = kk < kpw && clip < j.n_clips;
-    const bool first = s == 0, last = s == ns - 1;
-    const int64_t N = j.frames;
-    const int64_t nchunk = (N + CH - 1) / CH;
-    const float *x = valid ? j.in_ptrs[clip] : nullptr;
-    float *y = valid ? j.out_ptrs[clip] : nullptr;
-    const bq_f4 *src = first ? &in_buf[0][lane] : &sec_buf[0][(lane + 63) & 63];
-
-    const float *q = j.sos + 6 * s;
-    const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
-    float z0 = 0.0f, z1 = 0.0f;
-    float *st = (ST && valid) ? j.state + ((size_t)clip * ns + s) * 4 : nullptr;   // [z0 L,R][z1 L,R]
-    if (ST && st) { z0 = st[ch]; z1 = st[2 + ch]; }
-
-    bq_f4 pa[2 * G], pb[2 * G];                    // raw interleaved granules, chunks i and i + 1
-    auto load = [&](bq_f4 (&d)[2 * G], int64_t c) {
-        if (!(first && valid && c < nchunk)) return;
-        const float *xc = x + (size_t)2 * (size_t)(c * CH);
-        if ((c + 1) * CH <= N && (((uintptr_t)xc) & 15) == 0) {
-#pragma unroll
-            for (int g = 0; g < 2 * G; ++g) d[g] = ((gcf4 *)xc)[g];
-        } else {
-#pragma unroll
-            for (int g = 0; g < 2 * G; ++g)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    d[g][e] = (c * CH) * 2 + g * 4 + e < N * 2 ? xc[g * 4 + e] : 0.0f;
-        }
-    };
-    auto step = [&](int64_t i, bq_f4 (&cur)[2 * G]) {
-        if (first) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const bq_f4 u = cur[2 * g], w = cur[2 * g + 1];
-                in_buf[g][lane] = ch ? bq_f4{u[1], u[3], w[1], w[3]} : bq_f4{u[0], u[2], w[0], w[2]};
-            }
-        }
-        load(cur, i + 2);
-        const int64_t c = i - s;
-        bq_f4 v4[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) v4[g] = src[g * 64];
-        if (c >= 0 && c < nchunk) {
-            const bool tail = ST && st && (c + 1) * CH > N;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                bq_f4 r;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float v = v4[g][e];
-                    const float o = b0 * v + z0;          // sosfilt (_sosfilt.pyx) order
-                    if (!(tail && c * CH + g * 4 + e >= N)) {
-                        z0 = (b1 * v - a1 * o) + z1;
-                        z1 = b2 * v - a2 * o;
-                    }
-                    r[e] = o;
-                }
-                v4[g] = r;
-            }
-            if (!last) {
-#pragma unroll
-                for (int g = 0; g < G; ++g) sec_buf[g][lane] = v4[g];
-            } else if (valid) {
-                float *yc = y + (size_t)2 * (size_t)(c * CH) + ch;
-                if ((c + 1) * CH <= N) {
-#pragma unroll
-                    for (int g = 0; g < G; ++g)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) yc[(g * 4 + e) * 2] = v4[g][e];
-                } else {
-#pragma unroll
-                    for (int g = 0; g < G; ++g)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (c * CH + g * 4 + e < N) yc[(g * 4 + e) * 2] = v4[g][e];
-                }
-            }
-        }
-    };
-    load(pa, 0);
-    load(pb, 1);
-    const int64_t steps = nchunk + ns - 1;
-    for (int64_t i = 0; i < steps; i += 2) {   // cross-lane LDS hand-off: see k_biquad_lanes
-        step(i, pa);
-        __builtin_amdgcn_wave_barrier();
-        if (i + 1 < steps) step(i + 1, pb);
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (ST && st) { st[ch] = z0; st[2 + ch] = z1; }
 }
 
 constexpr int FIR_THREADS = 256;
@@ -366,31 +433,29 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
     if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
     if (j->n_clips == 0 || j->frames == 0) return 0;
 
-    // 64-frame chunks: half the per-chunk LDS hand-offs of 32 and one chunk
-    // more of compute to cover each prefetch (config 4: 24.06 -> 22.83 ms)
-    auto kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 64, true> : k_biquad_lanes<2, 64, true>)
-                         : (j->channels == 1 ? k_biquad_lanes<1, 64, false> : k_biquad_lanes<2, 64, false>);
-    int lpc = j->n_sos;                                // lanes per clip
-    XmhFxJob jj = *j;
-    jj.dev_flags = 0;
-#ifdef XM_FX_DEVKNOBS
-    // dev builds only (`make ablate`): A/B and attribution knobs.  XM_FX_DEV=1
-    // skips section 0's loads (wrong results by design), so the shipped
-    // library never reads these variables.
-    if (const char *c = getenv("XM_BQ_CH"); c && atoi(c) == 32)   // the previous chunk length
-        kern = j->state ? (j->channels == 1 ? k_biquad_lanes<1, 32, true> : k_biquad_lanes<2, 32, true>)
-                        : (j->channels == 1 ? k_biquad_lanes<1, 32, false> : k_biquad_lanes<2, 32, false>);
-    if (j->channels == 2 && getenv("XM_BQ_SPLIT")) {   // one channel per lane (measured slower)
-        kern = j->state ? k_biquad_split<32, true> : k_biquad_split<32, false>;
-        lpc = 2 * j->n_sos;
-    }
-    if (const char *d = getenv("XM_FX_DEV")) jj.dev_flags = atoi(d);
-#endif
-    const int kpw = 64 / lpc;
+    auto kern = j->channels == 2 ? (j->state ? k_biquad_pipe<2, true> : k_biquad_pipe<2, false>)
+                                 : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>);
+    const int kpw = std::min(64 / j->n_sos, BQ_KPW);
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    hipLaunchKernelGGL(kern, grid, dim3(64), 0, (hipStream_t)stream, jj);
+    static std::atomic<int> lds_set[4];            // per (C, ST) instantiation, set once per process
+    const int ki = (j->channels == 2) * 2 + (j->state != nullptr);
+    if (!lds_set[ki].load(std::memory_order_acquire)) {
+        if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BQ_LDS) !=
+            hipSuccess)
+            return -1001;
+        lds_set[ki].store(1, std::memory_order_release);
+    }
+    XmhFxJob jj = *j;
+    hipLaunchKernelGGL(kern, grid, dim3(128), BQ_LDS, (hipStream_t)stream, jj);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
+
+#ifdef XM_BQ_PROF
+extern "C" __attribute__((visibility("default"))) int xmh_dev_bq_prof(uint64_t *host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_prof), sizeof(g_bq_prof)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int xmh_launch_fx_fir(const XmhFxJob *j, void *stream)
 {

@@ -91,7 +91,7 @@ typedef struct XmhFxJob {
     int32_t n_sos;
     int32_t fir_len;
     const float *fir;              /* device fir_len taps */
-    int32_t dev_flags;             /* dev/attribution only (XM_FX_DEV env), 0 in the product */
+    int32_t reserved0;
     int32_t reserved;
     /* streaming state (xm_effects_process_stream; NULL for whole clips):
      * biquad: state[clip][section][z0,z1][channel], read at the start of the
