@@ -49,6 +49,22 @@ struct XmEffects;
  * f32 = y * 2^-15 (exact) of the saturated Q15 mix.  Output buffers and
  * output strides are then in elements of the output format. */
 #define XM_MIXER_OUT_CONVERT 1u
+/* XmMixerConfig.flags: the inputs are in the other sample format, converted in
+ * the kernels' load path.  F32 mixers read s16
+ * tracks as x * 2^-15 (exact); S16 mixers read f32 tracks as
+ * saturate16(rint(x * 32768)) (ties to even).  Input buffers and input
+ * strides are then in elements of the input format. */
+#define XM_MIXER_IN_CONVERT 2u
+/* XmMixerConfig.flags: planar PCM (stereo; mono is the same either way).  A
+ * track of frames_in frames is `channels` planes of frames_in samples (plane c
+ * = samples [c*frames_in, (c+1)*frames_in) from the track's start), a mix
+ * output `channels` planes of out_frames samples; track and mix strides keep
+ * their meaning (elements from one track / mix to the next).  The layout is
+ * read and written by the kernels' load and store paths, no transposes.
+ * IN_CONVERT and PLANAR apply to process_batch and process_strided, with or
+ * without per-track effects; the streaming, timeline and config-5 calls
+ * return XM_ENOSYS on such a handle. */
+#define XM_MIXER_PLANAR 4u
 
 typedef struct XmMixerConfig {
     int32_t in_rate;      /* Hz, every track (per-track rates: XmTrackDesc.in_rate) */
@@ -57,7 +73,7 @@ typedef struct XmMixerConfig {
     int32_t sample_fmt;   /* XmSampleFmt, input and output */
     int32_t mem_kind;     /* XmMemKind of the in/out pointers */
     int32_t device;       /* HIP device ordinal the handle runs on */
-    int32_t flags;        /* 0 or XM_MIXER_OUT_CONVERT */
+    int32_t flags;        /* 0 or XM_MIXER_OUT_CONVERT | XM_MIXER_IN_CONVERT | XM_MIXER_PLANAR */
     int32_t n_devices;    /* 0 or 1: one device; n > 1: devices device .. device+n-1 */
 } XmMixerConfig;
 

@@ -16,6 +16,33 @@ constexpr int GEN_THREADS = 256;
 constexpr int GEN_OPT = 4;                          // outputs per thread per block
 constexpr int GEN_CHUNK = GEN_THREADS * GEN_OPT;    // output frames per block
 
+// Input / output layouts and formats (XmhMixJob.io_flags, whole clips only).
+// Input sample (frame f, channel c) of a track of N frames: interleaved at
+// f*C + c, planar at c*N + f; in the mix format, or converted from the other
+// one (XMH_IO_IN_CONV): an f32 mix reads s16 as x * 2^-15 (exact), an s16
+// mix reads f32 as sat16(rint(x * 32768)).  Element size of the input:
+template <bool S16>
+XM_DEV int xm_in_elem(const XmhMixJob &j) { return ((j.io_flags & XMH_IO_IN_CONV) != 0) != S16 ? 2 : 4; }
+XM_DEV int64_t xm_in_idx(const XmhMixJob &j, int64_t f, int c, int C)
+{
+    return (j.io_flags & XMH_IO_IN_PLANAR) ? (int64_t)c * j.frames_in + f : f * C + c;
+}
+XM_DEV int64_t xm_out_idx(const XmhMixJob &j, int64_t m, int c, int C)
+{
+    return (j.io_flags & XMH_IO_OUT_PLANAR) ? (int64_t)c * j.frames_out + m : m * C + c;
+}
+// the sample as the f32 mix sees it
+XM_DEV float xm_in_f32(const XmhMixJob &j, const void *x, int64_t i)
+{
+    return (j.io_flags & XMH_IO_IN_CONV) ? (float)((const int16_t *)x)[i] * 0x1p-15f : ((const float *)x)[i];
+}
+// the sample as the s16 mix sees it
+XM_DEV int32_t xm_in_s16(const XmhMixJob &j, const void *x, int64_t i)
+{
+    return (j.io_flags & XMH_IO_IN_CONV) ? xm_round_sat16(((const float *)x)[i] * 32768.0f)
+                                         : (int32_t)((const int16_t *)x)[i];
+}
+
 // Block = (output chunk, mix).  For every track: stage the input frames the
 // chunk needs into LDS (zero outside [0, N) — equivalent to scipy's skip, see
 // DESIGN.md "zero padding"), then each thread forms its outputs tap by tap in
@@ -49,7 +76,14 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
 
     for (int tr = 0; tr < j.n_tracks; ++tr) {
         __syncthreads();
-        if (S16) {
+        if (j.io_flags) {                            // other input format / planar (whole clips: ib = 0)
+            const void *x = xm_track_ptr(j, b, tr, xm_in_elem<S16>(j));
+            for (int i = threadIdx.x; i < span * C; i += GEN_THREADS) {
+                const int64_t f = jlo + i / C;
+                const int64_t q = xm_in_idx(j, f, i % C, C);
+                tile[i] = (f >= 0 && f < N) ? (S16 ? (float)xm_in_s16(j, x, q) : xm_in_f32(j, x, q)) : 0.0f;
+            }
+        } else if (S16) {
             const int16_t *x = (const int16_t *)xm_track_ptr(j, b, tr, 2);
             for (int i = threadIdx.x; i < span * C; i += GEN_THREADS) {
                 int64_t f = jlo + i / C;
@@ -103,19 +137,21 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
         } else if (S16 && j.out_conv == 2) {
             float *y = (float *)xm_out_ptr(j, b, 4);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = (float)xm_sat16(acci[o][c]) * 0x1p-15f;
+            for (int c = 0; c < C; ++c) y[xm_out_idx(j, m - ob, c, C)] = (float)xm_sat16(acci[o][c]) * 0x1p-15f;
         } else if (S16) {
             int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = xm_sat16(acci[o][c]);
+            for (int c = 0; c < C; ++c) y[xm_out_idx(j, m - ob, c, C)] = xm_sat16(acci[o][c]);
         } else if (j.out_conv == 1) {
             int16_t *y = (int16_t *)xm_out_ptr(j, b, 2);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = (int16_t)xm_round_sat16(accf[o][c] * 32768.0f);
+            for (int c = 0; c < C; ++c)
+                y[xm_out_idx(j, m - ob, c, C)] = (int16_t)xm_round_sat16(accf[o][c] * 32768.0f);
         } else {
             float *y = (float *)xm_out_ptr(j, b, 4);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[(m - ob) * C + c] = accf[o][c] + 0.0f;  // -0 -> +0 (scipy acc starts at +0)
+            for (int c = 0; c < C; ++c)
+                y[xm_out_idx(j, m - ob, c, C)] = accf[o][c] + 0.0f;  // -0 -> +0 (scipy acc starts at +0)
         }
     }
 }
@@ -247,6 +283,45 @@ __global__ __launch_bounds__(MIX_THREADS) void k_mix_f32(XmhMixJob j)
     } else {
         for (int i = 0; i < SPT; ++i)
             if (s0 + i < total) y[i] = acc[i] + 0.0f;
+    }
+}
+
+// No-resample mix with input conversion and / or planar layouts (io_flags):
+// one thread per output frame, the same per-frame arithmetic as k_mix_s16 /
+// k_mix_f32 (gain at the frame, tracks in order, Q15 terms or f32 acc from
+// +0), the samples read and written element by element through the layout.
+// Consecutive threads take consecutive frames, so planar planes and
+// interleaved rows both stay coalesced.
+template <int C, bool S16>
+__global__ __launch_bounds__(MIX_THREADS) void k_mix_flex(XmhMixJob j)
+{
+    const int b = blockIdx.y;
+    const int64_t f = (int64_t)blockIdx.x * MIX_THREADS + threadIdx.x;
+    if (f >= j.frames_out) return;
+    float accf[C];
+    int32_t acci[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) { accf[c] = 0.0f; acci[c] = 0; }
+    for (int tr = 0; tr < j.n_tracks; ++tr) {
+        const void *x = xm_track_ptr(j, b, tr, xm_in_elem<S16>(j));
+        const XmhGain g = j.gains[tr];
+        if (S16) {
+            const int32_t gq = xm_gain_q15(g, f);
+#pragma unroll
+            for (int c = 0; c < C; ++c) acci[c] += xm_q15_term(xm_in_s16(j, x, xm_in_idx(j, f, c, C)), gq);
+        } else {
+            const float gf = xm_gain_f32(g, f);
+#pragma unroll
+            for (int c = 0; c < C; ++c) accf[c] = accf[c] + gf * xm_in_f32(j, x, xm_in_idx(j, f, c, C));
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int64_t i = xm_out_idx(j, f, c, C);
+        if (S16 && j.out_conv == 2) ((float *)xm_out_ptr(j, b, 4))[i] = (float)xm_sat16(acci[c]) * 0x1p-15f;
+        else if (S16) ((int16_t *)xm_out_ptr(j, b, 2))[i] = xm_sat16(acci[c]);
+        else if (j.out_conv == 1) ((int16_t *)xm_out_ptr(j, b, 2))[i] = (int16_t)xm_round_sat16(accf[c] * 32768.0f);
+        else ((float *)xm_out_ptr(j, b, 4))[i] = accf[c] + 0.0f;
     }
 }
 
@@ -382,6 +457,16 @@ extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
     if (j->frames_out == 0 || j->n_mix == 0) return 0;
     if (j->partial && !s16) return -22;   // XM_EINVAL: partials are the s16 (Q15) mix
     if (j->partial && j->out_conv) return -22;
+    if ((j->in_base || j->out_base) && j->io_flags) return -22;   // layouts / conversion: whole clips only
+    if (j->rs.L == j->rs.M && j->io_flags) {
+        dim3 grid((unsigned)((j->frames_out + MIX_THREADS - 1) / MIX_THREADS), (unsigned)j->n_mix);
+        int rc = s16 ? (C == 1 ? launch(k_mix_flex<1, true>, grid, MIX_THREADS, 0, s, *j)
+                               : launch(k_mix_flex<2, true>, grid, MIX_THREADS, 0, s, *j))
+                     : (C == 1 ? launch(k_mix_flex<1, false>, grid, MIX_THREADS, 0, s, *j)
+                               : launch(k_mix_flex<2, false>, grid, MIX_THREADS, 0, s, *j));
+        if (n_launches) *n_launches += 1;
+        return rc;
+    }
     if (j->rs.L == j->rs.M) {
         const int spt = s16 ? 8 : 4;
         const int64_t samples = j->frames_out * C;

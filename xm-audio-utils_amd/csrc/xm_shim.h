@@ -77,8 +77,13 @@ typedef struct XmhMixJob {
     /* output format conversion in the store epilogue (XM_MIXER_OUT_CONVERT):
      * 0 none; 1 f32 mix -> s16 out = sat16(rint(y * 32768)); 2 s16 mix -> f32 out = y * 2^-15 */
     int32_t out_conv;
-    int32_t reserved3;
+    /* input conversion and planar layouts (XM_MIXER_IN_CONVERT / PLANAR),
+     * whole-clip jobs only (in_base = out_base = 0): XMH_IO_* bits */
+    int32_t io_flags;
 } XmhMixJob;
+#define XMH_IO_IN_CONV    1   /* f32 mix reads s16 (x * 2^-15); s16 mix reads f32 (sat16(rint(x * 32768))) */
+#define XMH_IO_IN_PLANAR  2   /* track = C planes of frames_in samples */
+#define XMH_IO_OUT_PLANAR 4   /* mix output = C planes of frames_out samples */
 
 /* ---------- effects job ---------------------------------------------------- */
 typedef struct XmhFxJob {

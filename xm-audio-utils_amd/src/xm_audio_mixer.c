@@ -62,6 +62,23 @@ const XmTrackDesc *xm_mixer_tracks(const XmAudioMixer *m, int *n_tracks)
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
 
+/* input element size (XM_MIXER_IN_CONVERT reads the other format) */
+static int in_bytes(const XmAudioMixer *m)
+{
+    const int conv = (m->cfg.flags & XM_MIXER_IN_CONVERT) != 0;
+    return fmt_bytes(conv ? (m->cfg.sample_fmt == XM_FMT_S16 ? XM_FMT_F32 : XM_FMT_S16) : m->cfg.sample_fmt);
+}
+
+/* the flags only whole-clip batch calls implement (stereo planar; mono is
+ * planar and interleaved at once) */
+static int io_flags(const XmAudioMixer *m)
+{
+    int f = 0;
+    if (m->cfg.flags & XM_MIXER_IN_CONVERT) f |= XMH_IO_IN_CONV;
+    if ((m->cfg.flags & XM_MIXER_PLANAR) && m->cfg.channels == 2) f |= XMH_IO_IN_PLANAR | XMH_IO_OUT_PLANAR;
+    return f;
+}
+
 /* output element size (XM_MIXER_OUT_CONVERT writes the other format) */
 static int out_bytes(const XmAudioMixer *m)
 {
@@ -87,7 +104,8 @@ static int cfg_valid(const XmMixerConfig *cfg)
     return cfg && cfg->in_rate > 0 && cfg->out_rate > 0 && (cfg->channels == 1 || cfg->channels == 2) &&
            (cfg->sample_fmt == XM_FMT_S16 || cfg->sample_fmt == XM_FMT_F32) &&
            (cfg->mem_kind == XM_MEM_HOST || cfg->mem_kind == XM_MEM_DEVICE) && cfg->device >= 0 &&
-           !(cfg->flags & ~(int32_t)XM_MIXER_OUT_CONVERT) && cfg->n_devices >= 0 &&
+           !(cfg->flags & ~(int32_t)(XM_MIXER_OUT_CONVERT | XM_MIXER_IN_CONVERT | XM_MIXER_PLANAR)) &&
+           cfg->n_devices >= 0 &&
            cfg->n_devices <= XM_MAX_DEVICES;
 }
 
@@ -364,6 +382,7 @@ static void job_init(XmAudioMixer *m, XmhMixJob *j, size_t batch, size_t frames_
     j->rs.H = m->table.H_dev;
     j->rs.fast = m->table.fast;
     if (m->cfg.flags & XM_MIXER_OUT_CONVERT) j->out_conv = m->cfg.sample_fmt == XM_FMT_F32 ? 1 : 2;
+    j->io_flags = io_flags(m);
 }
 
 static int upload_gains(XmAudioMixer *m)
@@ -403,6 +422,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     rc = xmh_memcpy_h2d(ug, &unity_gain, sizeof unity_gain, m->stream);
     XmhMixJob r = *j0;
     r.out_conv = 0;   /* tracks stay f32 in scratch; the final mix converts */
+    r.io_flags = j0->io_flags & ~XMH_IO_OUT_PLANAR;   /* scratch is interleaved */
     r.n_tracks = 1;
     r.n_mix = (int32_t)ntot;
     r.gains = ug;
@@ -469,6 +489,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         x.rs.rm = 0;
         x.unity = 0;
         x.rs.fast = 0;
+        x.io_flags = j0->io_flags & XMH_IO_OUT_PLANAR;   /* reads the f32 interleaved scratch */
         rc = xmh_launch_mix(&x, m->stream, launches, &m->timing.fast_launches);
     }
     xmh_stream_sync(m->stream);
@@ -553,7 +574,7 @@ static int process_device(XmAudioMixer *m, const void *const *in, void *const *o
 {
     XmhMixJob j;
     job_init(m, &j, batch, frames_in);
-    const int elem = fmt_bytes(m->cfg.sample_fmt);
+    const int elem = in_bytes(m);
     int64_t ts = 0, ms = 0, os = 0, dummy = 0;
     const void *const *din = NULL;
     void *const *dout = NULL;
@@ -584,7 +605,7 @@ static int process_device(XmAudioMixer *m, const void *const *in, void *const *o
 static int process_host(XmAudioMixer *m, const void *const *in, void *const *out, size_t batch,
                         size_t frames_in)
 {
-    const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->n_tracks;
+    const int elem = in_bytes(m), C = m->cfg.channels, ntr = m->n_tracks;
     const size_t fout = xm_audio_mixer_out_frames(m, frames_in);
     const size_t in_track = frames_in * (size_t)C * (size_t)elem;
     const size_t out_mix = fout * (size_t)C * (size_t)out_bytes(m);
@@ -656,7 +677,7 @@ int xm_audio_mixer_process_partial_s16(XmAudioMixer *m, const void *in, ptrdiff_
     if (!m || (batch && (!in || !partial))) return XM_EINVAL;
     if (m->multi) return XM_ENOSYS;   /* config 5 on several devices: mix_spanning_s16 */
     if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || m->fx || m->mixed_rates ||
-        (m->cfg.flags & XM_MIXER_OUT_CONVERT))
+        (m->cfg.flags & XM_MIXER_OUT_CONVERT) || io_flags(m))
         return XM_ENOSYS;
     if (batch == 0) return XM_OK;
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
@@ -682,7 +703,8 @@ int xm_audio_mixer_finish_s16(XmAudioMixer *m, const int32_t *partials, int n_pa
                               size_t out_frames)
 {
     if (!m || n_parts < 1 || n_parts > XM_MAX_TRACKS) return XM_EINVAL;
-    if (m->multi || m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE) return XM_ENOSYS;
+    if (m->multi || m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || io_flags(m))
+        return XM_ENOSYS;
     if (batch == 0 || out_frames == 0) return XM_OK;
     if (!partials || !out || batch > (size_t)INT32_MAX) return XM_EINVAL;
     int rc = xmh_set_device(m->cfg.device);
@@ -711,7 +733,7 @@ int xm_audio_mixer_process_strided(XmAudioMixer *m, const void *in, ptrdiff_t in
                                                   batch, frames_in);
     if (m->cfg.mem_kind != XM_MEM_DEVICE) {
         /* host memory: expand to pointer arrays */
-        const int elem = fmt_bytes(m->cfg.sample_fmt);
+        const int elem = in_bytes(m);
         size_t ntr = (size_t)m->n_tracks;
         const void **ip = malloc(sizeof(void *) * batch * ntr);
         void **op = malloc(sizeof(void *) * batch);
@@ -772,6 +794,7 @@ int xm_audio_mixer_stream_begin(XmAudioMixer *m, size_t batch)
     if (!m || batch == 0 || batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
     if (m->multi) return xm_multi_stream_begin(m->multi, batch);
     if (m->fx || m->mixed_rates) return XM_ENOSYS;   /* effects: xm_effects_process_stream */
+    if (io_flags(m)) return XM_ENOSYS;               /* XM_MIXER_IN_CONVERT / PLANAR: whole-clip calls */
     int rc = xmh_set_device(m->cfg.device);
     if (rc) return rc;
     if ((rc = xmh_stream_sync(m->stream))) return rc;   /* a previous stream's copies */
@@ -799,7 +822,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
         return xm_multi_stream_step(m->multi, in, ts, ms, n, out, os, out_cap, frames_out, flush);
     }
     if (!m || !m->st_on || (n && !in) || !frames_out) return XM_EINVAL;
-    if (m->fx || m->mixed_rates) return XM_ENOSYS;   /* as stream_begin */
+    if (m->fx || m->mixed_rates || io_flags(m)) return XM_ENOSYS;   /* as stream_begin */
     if (m->n_tracks != m->st_ntr) return XM_EINVAL;   /* track list changed mid-stream */
     const int elem = fmt_bytes(m->cfg.sample_fmt), C = m->cfg.channels, ntr = m->st_ntr;
     const size_t batch = m->st_batch, rows = batch * (size_t)ntr, fb = (size_t)C * (size_t)elem;
@@ -1002,7 +1025,7 @@ int xm_audio_mixer_process_timeline(XmAudioMixer *m, const void *const *in, cons
                                     void *const *out, size_t batch, size_t out_frames)
 {
     if (!m || !place || (batch && (!in || !out))) return XM_EINVAL;
-    if (m->fx) return XM_ENOSYS;
+    if (m->fx || io_flags(m)) return XM_ENOSYS;
     if (batch == 0 || out_frames == 0) return XM_OK;
     if (m->multi) return xm_multi_process_timeline(m->multi, in, place, out, batch, out_frames);
     if (batch > (size_t)INT32_MAX / XM_MAX_TRACKS) return XM_EINVAL;
@@ -1068,7 +1091,8 @@ int xm_audio_mixer_mix_spanning_s16(XmAudioMixer *m, const void *const *in, ptrd
         return xm_multi_mix_spanning_s16(m->multi, in, in_track_stride, in_mix_stride, out, out_mix_stride, batch,
                                          frames_in);
     /* one device holds every track: no exchange, the plain mix */
-    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || (m->cfg.flags & XM_MIXER_OUT_CONVERT))
+    if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || (m->cfg.flags & XM_MIXER_OUT_CONVERT) ||
+        io_flags(m))
         return XM_ENOSYS;
     return xm_audio_mixer_process_strided(m, in[0], in_track_stride, in_mix_stride, out[0], out_mix_stride, batch,
                                           frames_in);

@@ -114,6 +114,12 @@ static void block(size_t batch, int n, int d, size_t *first, size_t *cnt)
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
 
+static int in_elem(const XmMixerConfig *c)
+{
+    const int conv = (c->flags & XM_MIXER_IN_CONVERT) != 0;
+    return fmt_bytes(conv ? (c->sample_fmt == XM_FMT_S16 ? XM_FMT_F32 : XM_FMT_S16) : c->sample_fmt);
+}
+
 static int out_elem(const XmMixerConfig *c)
 {
     const int conv = (c->flags & XM_MIXER_OUT_CONVERT) != 0;
@@ -296,7 +302,7 @@ static int t_strided(XmMulti *mu, int d, void *p)
     size_t f, c;
     block(a->batch, mu->n, d, &f, &c);
     if (!c) return XM_OK;
-    const char *in = (const char *)a->in1 + (ptrdiff_t)f * a->ms * fmt_bytes(mu->cfg.sample_fmt);
+    const char *in = (const char *)a->in1 + (ptrdiff_t)f * a->ms * in_elem(&mu->cfg);
     char *out = (char *)a->out1 + (ptrdiff_t)f * a->os * out_elem(&mu->cfg);
     return xm_audio_mixer_process_strided(mu->sub[d], in, a->ts, a->ms, out, a->os, c, a->frames);
 }
@@ -391,7 +397,7 @@ static int t_stream(XmMulti *mu, int d, void *p)
     XmStreamArg *a = p;
     a->got[d] = 0;
     if (!mu->st_cnt[d]) return XM_OK;
-    const char *in = a->in ? (const char *)a->in + (ptrdiff_t)mu->st_first[d] * a->ms * fmt_bytes(mu->cfg.sample_fmt)
+    const char *in = a->in ? (const char *)a->in + (ptrdiff_t)mu->st_first[d] * a->ms * in_elem(&mu->cfg)
                            : NULL;
     char *out = a->out ? (char *)a->out + (ptrdiff_t)mu->st_first[d] * a->os * out_elem(&mu->cfg) : NULL;
     if (a->flush) return xm_audio_mixer_stream_flush(mu->sub[d], out, a->os, a->cap, &a->got[d]);

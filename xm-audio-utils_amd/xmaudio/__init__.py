@@ -40,6 +40,8 @@ XM_OK, XM_EINVAL, XM_ENOMEM, XM_EDEVICE, XM_ECOMM, XM_ENOSYS = 0, -22, -12, -100
 XM_FMT_S16, XM_FMT_F32 = 1, 2
 XM_MEM_HOST, XM_MEM_DEVICE = 0, 1
 XM_MIXER_OUT_CONVERT = 1
+XM_MIXER_IN_CONVERT = 2
+XM_MIXER_PLANAR = 4
 XM_GAIN_RAMP, XM_GAIN_XFADE_OUT = 0, 1
 XM_EQ_PEAKING, XM_EQ_LOWSHELF, XM_EQ_HIGHSHELF, XM_EQ_LOWPASS, XM_EQ_HIGHPASS = range(5)
 FMT = {"s16": XM_FMT_S16, "f32": XM_FMT_F32}
@@ -219,11 +221,14 @@ class Mixer:
 
     def __init__(self, in_rate: int, out_rate: int, channels: int = 2, fmt: str = "f32",
                  mem: str = "host", device: int = 0, convert_out: bool = False, devices=None,
-                 n_devices: int = 0):
+                 n_devices: int = 0, convert_in: bool = False, planar: bool = False):
         """devices: a device list -> multi-device handle (xm_audio_mixer_create_multi);
-        n_devices > 1: devices device .. device+n-1 (XmMixerConfig.n_devices)."""
-        cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device,
-                            XM_MIXER_OUT_CONVERT if convert_out else 0, n_devices)
+        n_devices > 1: devices device .. device+n-1 (XmMixerConfig.n_devices).
+        convert_in: tracks in the other sample format (XM_MIXER_IN_CONVERT);
+        planar: planar PCM (XM_MIXER_PLANAR), arrays [..., channels, frames]."""
+        flags = ((XM_MIXER_OUT_CONVERT if convert_out else 0) | (XM_MIXER_IN_CONVERT if convert_in else 0) |
+                 (XM_MIXER_PLANAR if planar else 0))
+        cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device, flags, n_devices)
         st = C.c_int(0)
         if devices is not None:
             dl = (C.c_int * len(devices))(*devices)
@@ -234,8 +239,10 @@ class Mixer:
             raise XmError(st.value, "xm_audio_mixer_create")
         self.cfg = cfg
         self.fmt = FMT[fmt]
-        self.dtype = DTYPE[self.fmt]
-        self.out_dtype = (np.float32 if self.fmt == XM_FMT_S16 else np.int16) if convert_out else self.dtype
+        other = np.float32 if self.fmt == XM_FMT_S16 else np.int16
+        self.dtype = other if convert_in else DTYPE[self.fmt]          # input tracks
+        self.out_dtype = other if convert_out else DTYPE[self.fmt]
+        self.planar = planar
         self.channels = channels
         self.n_tracks = 1
 
@@ -272,14 +279,20 @@ class Mixer:
         return t
 
     def process(self, x: np.ndarray) -> np.ndarray:
-        """Host memory: x [batch, n_tracks, frames, channels] -> [batch, out_frames, channels]."""
+        """Host memory: x [batch, n_tracks, frames, channels] -> [batch, out_frames, channels]
+        (planar handles: [batch, n_tracks, channels, frames] -> [batch, channels, out_frames])."""
         x = np.ascontiguousarray(x, self.dtype)
-        assert x.ndim == 4 and x.shape[1] == self.n_tracks and x.shape[3] == self.channels, x.shape
-        B, ntr, N, Cc = x.shape
-        y = np.empty((B, self.out_frames(N), Cc), self.out_dtype)
+        assert x.ndim == 4 and x.shape[1] == self.n_tracks, x.shape
+        if self.planar:
+            B, ntr, Cc, N = x.shape
+            y = np.empty((B, Cc, self.out_frames(N)), self.out_dtype)
+        else:
+            B, ntr, N, Cc = x.shape
+            y = np.empty((B, self.out_frames(N), Cc), self.out_dtype)
+        assert Cc == self.channels, x.shape
         base, ts = x.ctypes.data, N * Cc * x.itemsize
         ins = (C.c_void_p * (B * ntr))(*[base + i * ts for i in range(B * ntr)])
-        ob, os_ = y.ctypes.data, y.shape[1] * Cc * y.itemsize
+        ob, os_ = y.ctypes.data, y[0].size * y.itemsize
         outs = (C.c_void_p * B)(*[ob + i * os_ for i in range(B)])
         _check(_lib.xm_audio_mixer_process_batch(self._h, ins, outs, B, N), "process_batch")
         return y
