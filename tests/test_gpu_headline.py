@@ -41,3 +41,90 @@ def test_headline_grid_first_last_mix(xm, gpu, B):
     assert bits_equal(got, ref)
     # no output frame was left unwritten anywhere in the batch
     assert not bool(y.isnan().any())
+
+
+@pytest.mark.parametrize("N", [48001, 160 * 300 + 1, 160 * 300 + 33, 4801, 441001])
+def test_fast_kernel_odd_lengths(xm, gpu, N):
+    """Odd frame counts stay on the fused kernel: the last chunk (frames N-1,
+    N) is loaded and frame N (the next track's first sample or padding) is
+    zeroed on the copy.  Lengths around a super-period edge and at a DMA
+    segment edge; every mix bit-compared with the oracle."""
+    from bench import RAMPS
+    B = 3
+    x, y = _run(xm, B, N, RAMPS)
+    ref, _ = CO.batch_resample_mix_f32(x.cpu().numpy(), RAMPS, 147, 160, threads=2)
+    assert bits_equal(y.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("N", [48001, 9601])
+def test_fast_split_odd_lengths(xm, gpu, N):
+    """Resample-only (config 2 split mode, 8 clips per pseudo-mix) with odd N:
+    per-clip outputs, no leakage between neighbouring clips."""
+    import torch
+    from bench import SEED
+    B = 16
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks([dict(gain0=1.0)])
+    F = m.out_frames(N)
+    x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+    xm.synth(x.data_ptr(), "f32", SEED, 77, B, 2, N)
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N)
+    t = m.timing()
+    assert t.fast_launches == 1, (t.n_launches, t.fast_launches)
+    xs = x.cpu().numpy()
+    got = y.cpu().numpy()
+    for b in (0, 7, 8, 15):
+        assert bits_equal(got[b], CO.resample_f32(xs[b], 147, 160)), b
+
+
+@pytest.mark.parametrize("N", [48000, 48001])
+def test_fast_kernel_pointer_tables(xm, gpu, N):
+    """Irregular per-track pointer tables stay on the fused kernel (one
+    buffer resource per mix based at its lowest track, per-track offsets
+    from the table): tracks in scattered order inside one tensor, plus one
+    mix whose tracks are separate allocations; outputs through a table too."""
+    import torch
+    from bench import RAMPS, SEED
+    B = 4
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks(RAMPS)
+    F = m.out_frames(N)
+    x = torch.empty((B, 8, N, 2), dtype=torch.float32, device="cuda")
+    xm.synth(x.data_ptr(), "f32", SEED, 300, B * 8, 2, N)
+    own = [x[B - 1, t].clone() for t in range(8)]             # the last mix: its own allocations
+    perm = [(3 * t + 5) % 8 for t in range(8)]
+    ins = [x[b, perm[t]].data_ptr() for b in range(B - 1) for t in range(8)] + [o.data_ptr() for o in own]
+    y = torch.full((B + 2, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    outs = [y[(5 * b) % (B + 2)].data_ptr() for b in range(B)]
+    torch.cuda.synchronize()
+    m.process_ptrs(ins, outs, B, N)
+    torch.cuda.synchronize()
+    t = m.timing()
+    assert t.fast_launches == 1, (t.n_launches, t.fast_launches)
+    xs = x.cpu().numpy()
+    got = y.cpu().numpy()
+    for b in range(B):
+        tracks = [xs[b, perm[t]] for t in range(8)] if b < B - 1 else [xs[b, t] for t in range(8)]
+        assert bits_equal(got[(5 * b) % (B + 2)], CO.resample_mix_f32(tracks, RAMPS, 147, 160)), b
+
+
+def test_fast_split_pointer_table(xm, gpu):
+    """Resample-only with an input pointer table (clips in a scattered order)."""
+    import torch
+    from bench import SEED
+    B, N = 16, 9600 + 1
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks([dict(gain0=1.0)])
+    F = m.out_frames(N)
+    x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+    xm.synth(x.data_ptr(), "f32", SEED, 900, B, 2, N)
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    perm = [(5 * b + 3) % B for b in range(B)]
+    m.process_ptrs([x[perm[b]].data_ptr() for b in range(B)], [y[b].data_ptr() for b in range(B)], B, N)
+    torch.cuda.synchronize()
+    assert m.timing().fast_launches == 1
+    xs, got = x.cpu().numpy(), y.cpu().numpy()
+    for b in (0, 5, 15):
+        assert bits_equal(got[b], CO.resample_f32(xs[perm[b]], 147, 160)), b

@@ -10,6 +10,15 @@ c4  per-GPU shard of config 4: 1024 clips = 128 mixes x 8 tracks, resample ->
     5-band RBJ EQ (biquad cascade) -> gain -> mix (8192 clips over 8 GPUs)
 c5  config 5 on this GPU: 512 mixes x 8 of their 64 s16 tracks -> int32 partial
     -> reduce-scatter over RCCL when launched with torchrun -> saturate
+Headline-shaped C-API variants (512 mixes x 8 stereo tracks x ~10 s, gain
+ramps, the kernel each one lands on in "kernel"):
+odd     frames_in 480001 (fused kernel, odd-length path)
+ptrs    irregular pointer table (tracks in scattered order: generic kernel)
+up      44.1k -> 48k fp32 (generic kernel)
+s16rs   48k -> 44.1k s16 Q15 (generic kernel)
+planar  48k -> 44.1k fp32, planar tracks and mixes (generic kernel)
+conv    48k -> 44.1k, s16 tracks into the fp32 mix (generic kernel)
+stream  the headline pushed in 8 blocks through stream_push (generic kernel)
 Unit: input samples (frames x channels x tracks) per second; roofline
 fraction = algorithmic bytes (inputs once + output once) / kernel time / 8 TB/s.
 Inputs are synthetic PCM generated in HBM (xm_synth_pcm), outside the timing.
@@ -138,6 +147,57 @@ def c5(a):
     xd.finish(rk)
 
 
+def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=False, conv=False,
+           stream=False):
+    B, ntr = a.mixes, 8
+    m = xm.Mixer(fi, fo, 2, fmt, mem="device", planar=planar, convert_in=conv)
+    m.set_tracks(Q15_RAMPS if fmt == "s16" else RAMPS)
+    F = m.out_frames(N)
+    ifmt = "s16" if (fmt == "s16") != conv else "f32"
+    isz = 2 if ifmt == "s16" else 4
+    osz = 2 if fmt == "s16" else 4
+    x = torch.empty((B, ntr, N, 2), dtype=torch.int16 if ifmt == "s16" else torch.float32, device="cuda")
+    y = torch.empty((B, F, 2), dtype=torch.int16 if fmt == "s16" else torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), ifmt, SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
+    m.set_stream(s.cuda_stream)
+    if ptrs:
+        # every mix's tracks in a scattered order: no common stride
+        perm = [(5 * t + 3) % ntr for t in range(ntr)]
+        ins = [x[b, perm[t]].data_ptr() for b in range(B) for t in range(ntr)]
+        outs = [y[b].data_ptr() for b in range(B)]
+        step = lambda: m.process_ptrs(ins, outs, B, N)   # noqa: E731
+    elif stream:
+        nb = 8
+        blk = (N + nb - 1) // nb
+        ys = torch.empty((B, F + 64, 2), dtype=y.dtype, device="cuda")
+
+        def step():
+            m.stream_begin(B)
+            got = 0
+            for i in range(nb):
+                lo, hi = i * blk, min(N, (i + 1) * blk)
+                got += m.stream_push_strided(x[0, 0, lo:].data_ptr(), N * 2, ntr * N * 2, hi - lo,
+                                             ys[0, got:].data_ptr(), (F + 64) * 2, F + 64 - got)
+            m.stream_flush_strided(ys[0, got:].data_ptr(), (F + 64) * 2, F + 64 - got)
+    else:
+        step = lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)  # noqa: E731
+    w, k = timed(step, a.steps, a.warmup, s)
+    fast = m.timing().fast_launches
+    report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix",
+           B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m,
+           kernel="k_rs147_mix" if fast else "generic")
+
+
+def odd(a): _shape(a, "odd", N=480001)
+def ptrs(a): _shape(a, "ptrs", ptrs=True)
+def up(a): _shape(a, "up", fi=44100, fo=48000, N=441000)
+def s16rs(a): _shape(a, "s16rs", fmt="s16")
+def planar(a): _shape(a, "planar", planar=True)
+def conv(a): _shape(a, "conv", conv=True)
+def stream(a): _shape(a, "stream", stream=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("which", nargs="*", default=["c2", "c3", "c4"])
@@ -147,6 +207,7 @@ def main():
     ap.add_argument("--mixes3", type=int, default=1024)
     ap.add_argument("--mixes4", type=int, default=128)
     ap.add_argument("--mixes5", type=int, default=512)
+    ap.add_argument("--mixes", type=int, default=512, help="headline-shaped variants")
     a = ap.parse_args()
     for w in a.which:
         globals()[w](a)

@@ -80,6 +80,10 @@ typedef struct XmhMixJob {
     /* input conversion and planar layouts (XM_MIXER_IN_CONVERT / PLANAR),
      * whole-clip jobs only (in_base = out_base = 0): XMH_IO_* bits */
     int32_t io_flags;
+    int32_t reserved4;
+    /* host copy of in_ptrs (same n_mix*n_tracks device pointers), or NULL:
+     * lets the launcher check a table's span for the fused kernel */
+    const void *const *in_ptrs_host;
 } XmhMixJob;
 #define XMH_IO_IN_CONV    1   /* f32 mix reads s16 (x * 2^-15); s16 mix reads f32 (sat16(rint(x * 32768))) */
 #define XMH_IO_IN_PLANAR  2   /* track = C planes of frames_in samples */

@@ -481,6 +481,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         XmhMixJob x = *j0;
         x.in = cur ? scratch2 : scratch;
         x.in_ptrs = NULL;
+        x.in_ptrs_host = NULL;
         x.in_track_stride = (int64_t)per_track;
         x.in_mix_stride = (int64_t)(per_track * (size_t)ntr);
         x.frames_in = j0->frames_out;
@@ -591,6 +592,7 @@ static int process_device(XmAudioMixer *m, const void *const *in, void *const *o
         j.in_mix_stride = ms;
     } else {
         j.in_ptrs = din;
+        j.in_ptrs_host = in;
     }
     if (out_strided) {
         j.out = out[0];

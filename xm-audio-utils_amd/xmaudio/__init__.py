@@ -292,7 +292,7 @@ class Mixer:
         assert Cc == self.channels, x.shape
         base, ts = x.ctypes.data, N * Cc * x.itemsize
         ins = (C.c_void_p * (B * ntr))(*[base + i * ts for i in range(B * ntr)])
-        ob, os_ = y.ctypes.data, y[0].size * y.itemsize
+        ob, os_ = y.ctypes.data, int(np.prod(y.shape[1:])) * y.itemsize
         outs = (C.c_void_p * B)(*[ob + i * os_ for i in range(B)])
         _check(_lib.xm_audio_mixer_process_batch(self._h, ins, outs, B, N), "process_batch")
         return y
