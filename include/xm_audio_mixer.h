@@ -9,7 +9,8 @@
  * freep / strerror), plus a strided form and a stream hook for callers whose
  * buffers already live in HBM.  Arithmetic: xm_audio_common.h.
  *
- * Data layout: each track / mix is interleaved PCM, frames x channels.
+ * Data layout: each track / mix is interleaved PCM, frames x channels
+ * (channel planes with XM_MIXER_PLANAR).
  * One "mix" = n_tracks input tracks -> one output of out_frames frames.
  *
  * Threading: a handle is not re-entrant (one caller thread per handle);
