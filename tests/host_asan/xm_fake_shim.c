@@ -218,6 +218,14 @@ int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fas
     return 0;
 }
 
+/* the fused kernel's streaming windows: not modelled here, the host falls
+ * back to the generic window job */
+int xmh_launch_mix_window(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
+{
+    (void)j; (void)stream; (void)n_launches; (void)n_fast;
+    return -1003;
+}
+
 int xmh_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
 {
     (void)stream;

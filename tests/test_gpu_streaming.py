@@ -217,3 +217,52 @@ def test_stream_mixed_rates_mid_stream(xm, gpu):
     with pytest.raises(xm.XmError) as e:
         m.stream_push(np.zeros((1, 2, 100, 2), np.float32))
     assert e.value.code == xm.XM_ENOSYS
+
+
+@pytest.mark.parametrize("pattern", ["big_ragged", "sp_edges", "one_block"])
+def test_stream_fused_window_path(xm, gpu, pattern):
+    """48k->44.1k stereo 8-track streams run their super-period-aligned bulk
+    on the fused kernel (a window job: input at the window frame of the
+    first aligned output, 32 real lead-in frames, ramps shifted) and the head
+    before it on the generic kernel; any split equals the whole-signal call."""
+    N = 48000 + 77
+    x = np.stack([np.stack([O.gen_f32(SEED, 6100 + 8 * b + t, 2, N) for t in range(8)]) for b in range(2)])
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks(RAMPS8)
+    want = m.process(x)
+    sizes = {"big_ragged": _blocks(N, [7001, 1, 0, 12345, 160 * 30 + 1, 3]),
+             "sp_edges": _blocks(N, [160 * 5, 160 * 20 + 32, 160 * 7 - 1, 160 * 40]),
+             "one_block": [N]}[pattern]
+    m.stream_begin(2)
+    outs, p, fast = [], 0, 0
+    for n in sizes:
+        outs.append(m.stream_push(x[:, :, p:p + n]))
+        fast += m.timing().fast_launches
+        p += n
+    outs.append(m.stream_flush())
+    fast += m.timing().fast_launches
+    assert fast >= 1, "the fused kernel never ran"
+    assert bits_equal(np.concatenate(outs, axis=1), want)
+
+
+def test_stream_fused_window_split_mode(xm, gpu):
+    """1-track unity-gain streams of 16 clips (split mode) in blocks; 9 clips
+    (a remainder) stay on the generic kernel, with the same bits."""
+    N, B = 9600 * 3 + 5, 16
+    x = np.stack([O.gen_f32(SEED, 6200 + b, 2, N)[None] for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "f32")
+    m.set_tracks([dict(gain0=1.0)])
+    want = m.process(x)
+    m.stream_begin(B)
+    outs, p, fast = [], 0, 0
+    for n in _blocks(N, [9000, 7, 10000]):
+        outs.append(m.stream_push(x[:, :, p:p + n]))
+        fast += m.timing().fast_launches
+        p += n
+    outs.append(m.stream_flush())
+    assert fast >= 1
+    assert bits_equal(np.concatenate(outs, axis=1), want)
+    x9 = x[:9]
+    m.stream_begin(9)
+    o9 = [m.stream_push(x9[:, :, :15000]), m.stream_push(x9[:, :, 15000:]), m.stream_flush()]
+    assert bits_equal(np.concatenate(o9, axis=1), want[:9])

@@ -80,7 +80,10 @@ typedef struct XmhMixJob {
     /* input conversion and planar layouts (XM_MIXER_IN_CONVERT / PLANAR),
      * whole-clip jobs only (in_base = out_base = 0): XMH_IO_* bits */
     int32_t io_flags;
-    int32_t reserved4;
+    /* 1: a streaming window for the fused kernel (xmh_launch_mix_window): in
+     * points at the input frame of output 0 and the 32 frames before it are
+     * real samples, not padding */
+    int32_t window;
     /* host copy of in_ptrs (same n_mix*n_tracks device pointers), or NULL:
      * lets the launcher check a table's span for the fused kernel */
     const void *const *in_ptrs_host;
@@ -154,6 +157,11 @@ const char *xmh_arch_name(void);
  * made to *n_launches and, if the fused 147/160 kernel took the job, 1 to
  * *n_fast (either pointer may be NULL) */
 int xmh_launch_mix(const XmhMixJob *job, void *stream, int *n_launches, int *n_fast);
+/* the fused kernel only, for a streaming window job (job->window = 1, or 0
+ * for the window that starts at the signal's frame 0); XM_ENOSYS (-1003)
+ * when the job is not its shape (the caller then runs the window through the
+ * generic kernel with in_base / out_base) */
+int xmh_launch_mix_window(const XmhMixJob *job, void *stream, int *n_launches, int *n_fast);
 int xmh_launch_fx(const XmhFxJob *job, void *stream, int *n_launches);
 /* timeline mix: out[m] = ordered sum over tracks of g_tr(m) * x_tr[m - place_tr.offset],
  * x_tr zero outside [0, place_tr.len); in_ptrs[b*n_tracks+tr] are the (resampled)

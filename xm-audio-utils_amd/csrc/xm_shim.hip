@@ -240,6 +240,13 @@ int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fas
     return xmh_launch_mix_generic(j, stream, n_launches);
 }
 
+int xmh_launch_mix_window(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
+{
+    const int rc = xmh_launch_mix_fast(j, stream, n_launches);
+    if (!rc && n_fast) *n_fast += 1;
+    return rc;
+}
+
 int xmh_launch_fx(const XmhFxJob *j, void *stream, int *n_launches)
 {
     int rc;

@@ -815,6 +815,44 @@ size_t xm_audio_mixer_stream_out_frames(const XmAudioMixer *m, size_t frames_in,
     return e > m->st_out ? (size_t)(e - m->st_out) : 0;
 }
 
+/* Streaming through the fused 147/160 kernel: the outputs of this release
+ * from the first super-period boundary ob_al = 147*ceil(out_base/147) on are
+ * one window job -- input pointer at the window's frame a0 = 160*ob_al/147,
+ * frames_in = R - a0 (frames past R read as zero, as the final flush needs;
+ * a non-final release never reads them), output pointer and gain ramps
+ * shifted by ob_al -- and the 32 frames before a0 are real samples
+ * (job->window; the window keeps them, st_step step 3).  On success *j is cut
+ * to the outputs before ob_al for the generic kernel; when the fused kernel
+ * does not take the job, *j is left whole. */
+static int st_fast_part(XmAudioMixer *m, XmhMixJob *j, int64_t R, const char *win, size_t fb, int *launches)
+{
+    const int64_t L = m->table.d.L, M = m->table.d.M;
+    if (L != 147 || M != 160 || !m->table.fast || j->io_flags || j->out_conv) return XM_OK;
+    const int64_t ob = j->out_base, oe = ob + j->frames_out;
+    const int64_t ob_al = (ob + L - 1) / L * L, a0 = ob_al / L * M;
+    if (oe - ob_al < 4 * L || a0 >= R || (a0 > 0 && a0 - 32 < m->st_w0)) return XM_OK;   /* too small to pay */
+    XmhGain g[XM_MAX_TRACKS];
+    for (int t = 0; t < m->n_tracks; ++t) {
+        g[t] = m->gains[t];
+        g[t].start -= ob_al;   /* the ramps are functions of n - start */
+    }
+    XmhMixJob w = *j;
+    w.in = win + (size_t)(a0 - m->st_w0) * fb;
+    w.frames_in = R - a0;
+    w.frames_out = oe - ob_al;
+    w.in_base = w.out_base = 0;
+    w.out = (char *)j->out + (size_t)(ob_al - ob) * (size_t)m->cfg.channels * (size_t)out_bytes(m);
+    w.gains_host = g;
+    w.rs.fast = m->table.fast;
+    w.window = a0 > 0;
+    w.unity = m->unity;
+    const int rc = xmh_launch_mix_window(&w, m->stream, launches, &m->timing.fast_launches);
+    if (rc == XM_ENOSYS) return XM_OK;   /* not the fused kernel's shape: all generic */
+    if (rc) return rc;
+    j->frames_out = ob_al - ob;          /* the head before the first boundary */
+    return XM_OK;
+}
+
 static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, size_t n, void *out,
                    ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush)
 {
@@ -888,7 +926,14 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
         j.rs.fast = 0;
         j.out = host ? m->d_out : out;
         j.out_mix_stride = host ? (int64_t)(nout * (size_t)C) : (int64_t)os;
-        rc = run_job(m, &j);
+        int launches = 0;
+        rc = xmh_event_record(m->ev[2], m->stream);
+        if (!rc) rc = st_fast_part(m, &j, R, win, fb, &launches);   /* the super-period-aligned bulk */
+        if (!rc && j.frames_out)                                   /* the rest: generic kernel */
+            rc = xmh_launch_mix(&j, m->stream, &launches, &m->timing.fast_launches);
+        m->timing.n_launches += launches;
+        if (!rc) rc = xmh_event_record(m->ev[3], m->stream);
+        if (!rc) m->ev_done = 1;
         if (!rc && host)
             rc = xmh_memcpy2d(out, (size_t)os * (size_t)out_bytes(m), m->d_out, nout * ofb, nout * ofb, batch,
                               m->stream);
@@ -899,8 +944,11 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     }
     m->st_out = mend;
     /* 3) drop the frames no later output reads (move the rest to the other buffer) */
-    int64_t w0 = st_first_needed(m, mend);
+    /* + the fused kernel's 32-frame lead-in (147/160 only: the no-resample
+     * kernels read the window from its first frame) */
+    int64_t w0 = st_first_needed(m, mend) - (m->table.d.L == 147 && m->table.d.M == 160 ? 32 : 0);
     if (w0 > R) w0 = R;
+    if (w0 < m->st_w0) w0 = m->st_w0;
     if (w0 > m->st_w0 && !flush) {
         const size_t left = (size_t)(R - w0);
         if (left)
