@@ -44,7 +44,9 @@ XM_API XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status);
 /* Host-memory chain on device 0 (SURVEY.md §8(b) form; n_devices must be 1). */
 XM_API XmEffects *xm_effects_create(int rate, int channels, int n_devices);
 
-/* sos = {b0, b1, b2, a0, a1, a2}; a0 must be 1 (as scipy sosfilt requires). */
+/* sos = {b0, b1, b2, a0, a1, a2}; a0 must be 1 (as scipy sosfilt requires).
+ * A chain holds up to 128 effects (XM_ENOMEM beyond); consecutive biquads run
+ * as one cascade of up to 64 sections per pass over the clip. */
 XM_API int xm_effects_add_biquad(XmEffects *e, const float sos[6]);
 
 /* RBJ audio-EQ-cookbook section designed in fp64 and cast to fp32.

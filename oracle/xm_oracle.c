@@ -181,9 +181,10 @@ void xo_resample_mix_s16(const float *H, int L, int M, int T, int rm,
 /* ---- effects: scipy sosfilt (TDF-II) and upfirdn order --------------- */
 void xo_biquad_f32(const float *sos, int nsec, const float *x, size_t N, int C, float *y)
 {
+    float (*z)[2] = calloc((size_t)(nsec > 0 ? nsec : 1), sizeof *z);   /* any cascade length */
+    if (!z) abort();
     for (int c = 0; c < C; ++c) {
-        float z[64][2];
-        memset(z, 0, sizeof z);
+        memset(z, 0, sizeof *z * (size_t)(nsec > 0 ? nsec : 1));
         for (size_t n = 0; n < N; ++n) {
             float v = x[n * C + c];
             for (int s = 0; s < nsec; ++s) {
@@ -196,6 +197,7 @@ void xo_biquad_f32(const float *sos, int nsec, const float *x, size_t N, int C, 
             y[n * C + c] = v;
         }
     }
+    free(z);
 }
 
 void xo_fir_f32(const float *h, int K, const float *x, size_t N, int C, float *y)

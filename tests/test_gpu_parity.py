@@ -310,17 +310,18 @@ def test_errors(xm, gpu):
         e2.add_biquad([1, 0, 0, 2, 0, 0])   # a0 != 1
 
 
-@pytest.mark.parametrize("n_sos", [1, 2, 5, 8, 15])
+@pytest.mark.parametrize("n_sos", [1, 2, 5, 8, 15, 16, 40, 64, 70])
 @pytest.mark.parametrize("channels", [1, 2])
 def test_biquad_cascade_shapes(xm, gpu, n_sos, channels):
     """Section-pipelined biquad kernel (lane = clip x section): every cascade
-    length up to XM_MAX_SOS, more clips than one wave holds, ragged lengths
+    length up to XM_MAX_SOS = 64 in one pass (70: split in two), more clips
+    than one workgroup holds, ragged lengths
     around the 64-granule chunk (128 stereo / 256 mono frames: whole chunks,
     a partial last chunk, one frame past a chunk), bit-compared with the C
     oracle (sosfilt order)."""
     z = golden("effects.npz")
     rng = np.random.default_rng(n_sos * 10 + channels)
-    sos = np.concatenate([z["sos"]] * 3)[:n_sos]
+    sos = np.concatenate([z["sos"]] * (n_sos // len(z["sos"]) + 1))[:n_sos]   # > 64: the stager splits
     e = xm.Effects(48000, channels)
     for s in sos:
         e.add_biquad(s)

@@ -19,7 +19,7 @@
 
 namespace {
 
-constexpr int BQ_MAXSEC = 15;   // XM_MAX_SOS (src/xm_internal.h): >= 4 clips per workgroup
+constexpr int BQ_MAXSEC = 64;   // XM_MAX_SOS (src/xm_internal.h): a cascade fills at most one wave of lanes
 
 // Section-pipelined cascade.  The recurrence of one section is serial in
 // time, so the only parallelism that keeps sosfilt's rounding is across

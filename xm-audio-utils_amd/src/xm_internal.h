@@ -10,9 +10,9 @@
 #include "../csrc/xm_shim.h"
 
 #define XM_MAX_TRACKS 64
-#define XM_MAX_SOS 15   /* one wave per section + a loader wave <= 1024 threads (csrc/xm_fx.hip) */
+#define XM_MAX_SOS 64   /* one lane per (clip, section) in one wave (csrc/xm_fx.hip k_biquad_pipe) */
 #define XM_MAX_FIR 4096
-#define XM_MAX_EFFECTS 32
+#define XM_MAX_EFFECTS 128   /* biquad sections + FIR stages per chain */
 
 /* Cached device resample table for one reduced ratio. */
 typedef struct XmTable {
