@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 [ -n "$2" ] && export XM_AUDIO_LIB=$2
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT"
-P2="SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_IFETCH"
+P2="SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE SQ_IFETCH"
 for k in 1 2; do
   eval C=\$P$k
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d $OUT/p$k -o run --output-format csv -- python3 tools/dev/bq_load.py > $OUT/p$k.log 2>&1 || { tail -5 $OUT/p$k.log; exit 1; }

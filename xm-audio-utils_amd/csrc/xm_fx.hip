@@ -105,7 +105,8 @@ __device__ __forceinline__ bq_f4 bq_step2(bq_f4 v4, bq_f2 &z0, bq_f2 &z1, bq_f2 
 
 constexpr int BQ_G = 64;     // granules per chunk = lanes per DMA instruction
 constexpr int BQ_KPW = 16;   // clips per wave at most (16 DMA + 16 stores per step)
-constexpr size_t BQ_LDS = (size_t)(64 + 4 * BQ_KPW) * (BQ_G + 1) * 16;   // 133,120 B
+constexpr int BQ_RP = 80;    // granules per input / output row: 65 + up to 15 of bank skew
+constexpr size_t BQ_LDS = ((size_t)4 * BQ_KPW * BQ_RP + 64 * (BQ_G + 1)) * 16;   // 148,480 B
 
 #ifdef XM_BQ_PROF
 __device__ uint64_t g_bq_prof[4096];   // dev: per-workgroup cycles (compute wave: chunk, barrier wait)
@@ -122,16 +123,26 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
     constexpr int G = BQ_G;
     constexpr int FPL = 4 / C;                     // frames per 16-B granule
     constexpr int CH = G * FPL;                    // frames per chunk
-    constexpr uint32_t ROWB = (G + 1) * 16, PARB = BQ_KPW * ROWB;
-    // dynamic LDS (BQ_LDS bytes), rows padded by one granule:
-    //   inb[parity][clip][granule]   input chunks (DMA targets, below 64 KB)
-    //   outb[parity][clip][granule]  the last sections' output chunks
-    //   sec[lane][granule]           the other sections' output chunks
+    // dynamic LDS (BQ_LDS bytes), in granules:
+    //   inb rows  [parity][clip], BQ_RP apart   input chunks (DMA targets, below 64 KB)
+    //   outb rows [parity][clip], BQ_RP apart   the last sections' output chunks
+    //   sec[lane][granule], rows G + 1 apart     the other sections' output chunks
+    // sec rows land on successive 16-B bank slots (65 = 1 mod 16), so a wave's
+    // 64 reads of sec[L-1][g] (and writes of sec[L][g]) are conflict-free.  The
+    // inb / outb row of clip k is skewed to the bank slot of the sec row its
+    // lane would otherwise use (section 0 reads "row L - 1", the last section
+    // writes "row L"), which keeps the mixed accesses conflict-free too (PMC
+    // without the skew: 43 % of LDS cycles were bank conflicts).
     extern __shared__ bq_f4 bq_lds[];
-    bq_f4 (*inb)[BQ_KPW][G + 1] = (bq_f4 (*)[BQ_KPW][G + 1])bq_lds;
-    bq_f4 (*outb)[BQ_KPW][G + 1] = (bq_f4 (*)[BQ_KPW][G + 1])(bq_lds + 2 * BQ_KPW * (G + 1));
-    bq_f4 (*sec)[G + 1] = (bq_f4 (*)[G + 1])(bq_lds + 4 * BQ_KPW * (G + 1));
     const int ns = j.n_sos;
+    constexpr int SEC0 = 4 * BQ_KPW * BQ_RP;      // first sec row, granules (a multiple of 16)
+    bq_f4 (*sec)[G + 1] = (bq_f4 (*)[G + 1])(bq_lds + SEC0);
+    auto inb_row = [&](int p, int k) __attribute__((always_inline)) {
+        return (p * BQ_KPW + k) * BQ_RP + ((k * ns - 1) * (G + 1) & 15);
+    };
+    auto outb_row = [&](int p, int k) __attribute__((always_inline)) {
+        return ((2 + p) * BQ_KPW + k) * BQ_RP + ((k * ns + ns - 1) * (G + 1) & 15);
+    };
     const int kpw = min(64 / ns, BQ_KPW);          // clips per workgroup
     const int lane = threadIdx.x & 63;
     const int clip0 = blockIdx.x * kpw;
@@ -171,13 +182,13 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
             dy[k] = (uint32_t)(bcast(yl, k) - ymin) + (uint32_t)lane * 16u;
         }
         const uint32_t loff = (uint32_t)lane * 16u;
-        const uint32_t inb0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)&inb[0][0][0]);
+        const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)bq_lds);
 
         // input chunk c of every clip -> inb[c & 1]: one LDS-DMA instruction per
         // clip (64 lanes x 16 B = the clip's whole chunk, straight into its row)
         auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
             if (c >= nchunk) return;
-            const uint32_t dst = inb0 + (uint32_t)(c & 1) * PARB;
+            const int par = (int)(c & 1);
             if (c < nfull) {
                 const uint64_t cbb = (uint64_t)c * CH * C * 4;
                 if (narrow) {
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
                         if (k >= nclip) break;     // wave-uniform
                         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
                                      :
-                                     : "s"(dst + (uint32_t)k * ROWB), "v"(dx[k]), "s"(xmin + cbb)
+                                     : "s"(lds0 + (uint32_t)inb_row(par, k) * 16u), "v"(dx[k]), "s"(xmin + cbb)
                                      : "memory", "m0");
                     }
                 } else {
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
                         if (k >= nclip) break;
                         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
                                      :
-                                     : "s"(dst + (uint32_t)k * ROWB), "v"(loff), "s"(bcast(xl, k) + cbb)
+                                     : "s"(lds0 + (uint32_t)inb_row(par, k) * 16u), "v"(loff), "s"(bcast(xl, k) + cbb)
                                      : "memory", "m0");
                     }
                 }
@@ -211,7 +222,7 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     if (f0 * C + e < N * C) v[e] = ((gcf *)x)[e];
-                inb[c & 1][k][lane] = v;
+                bq_lds[inb_row(par, k) + lane] = v;
             }
         };
         // the last sections' chunk c (in outb[p]) -> HBM
@@ -219,7 +230,7 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
             if (c < 0 || c >= nchunk) return;
             bq_f4 sv[BQ_KPW];
 #pragma unroll
-            for (int k = 0; k < BQ_KPW; ++k) sv[k] = outb[p][min(k, nclip - 1)][lane];
+            for (int k = 0; k < BQ_KPW; ++k) sv[k] = bq_lds[outb_row(p, min(k, nclip - 1)) + lane];
             if (c < nfull) {
                 const uint64_t cbb = (uint64_t)c * CH * C * 4;
 #pragma unroll
@@ -288,8 +299,8 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
         // the last chunk's frames past N are zero padding: with a state to
         // carry they must not advance the recurrence
         const bool tail = ST && st && act && (c + 1) * CH > N;
-        const bq_f4 *src = s ? srow : &inb[i & 1][kc][0];
-        bq_f4 *dst = last ? &outb[i & 1][kc][0] : &sec[lane][0];
+        const bq_f4 *src = s ? srow : bq_lds + inb_row((int)(i & 1), kc);
+        bq_f4 *dst = last ? bq_lds + outb_row((int)(i & 1), kc) : &sec[lane][0];
         // fully unrolled over the chunk: granule g + 2 is read while granule
         // g is filtered, so the LDS latency hides behind two granules
         bq_f4 n0 = src[0], n1 = src[1];
