@@ -326,7 +326,9 @@ def test_biquad_cascade_shapes(xm, gpu, n_sos, channels):
     for s in sos:
         e.add_biquad(s)
     ch = 256 // channels
-    kpw = min(64 // n_sos, 16)
+    # clips per workgroup: k_biquad_mf (<= 16 sections, (16 / n_sos) groups
+    # of 4 / channels clips) or k_biquad_pipe (64 / n_sos)
+    kpw = min(16 // n_sos * (4 // channels), 16) if n_sos <= 16 else min(64 // n_sos, 16)
     for B, N in [(1, 1), (3, 31), (2 * kpw + 1, 33), (17, 1000), (5, ch), (kpw, 2 * ch), (3, 3 * ch + 1),
                  (kpw + 1, 4 * ch - 1)]:
         x = (rng.standard_normal((B, N, channels)) * 0.5).astype(np.float32)
@@ -401,6 +403,41 @@ def test_partial_errors(xm, gpu):
     with pytest.raises(xm.XmError) as e:
         h.finish_s16(1, 1, 0, 2, 1, 2, 1, 1)
     assert e.value.code == xm.XM_ENOSYS
+
+
+@pytest.mark.parametrize("n_sos", [5, 20])
+@pytest.mark.parametrize("channels", [1, 2])
+def test_biquad_silence_zeros_and_denormals(xm, gpu, n_sos, channels):
+    """Signed zeros, exact silence and denormals through the cascade: bursts
+    followed by long silences, so every section's state decays through the
+    denormal range to zero; -0 and denormal input samples; a clip of pure
+    -0.  The feed-forward products (matrix core in k_biquad_mf, VALU in
+    k_biquad_pipe for 20 sections) must keep IEEE signed zeros and gradual
+    underflow: bit-compared with the C oracle."""
+    z = golden("effects.npz")
+    sos = np.concatenate([z["sos"]] * (n_sos // len(z["sos"]) + 1))[:n_sos]
+    e = xm.Effects(48000, channels)
+    for s in sos:
+        e.add_biquad(s)
+    rng = np.random.default_rng(4242 + n_sos + channels)
+    B, N = 6, 60000
+    x = np.zeros((B, N, channels), np.float32)
+    x[0, :500] = rng.standard_normal((500, channels)) * 0.5
+    x[1, 100:101] = 1.0                                   # an impulse, then 59899 frames of silence
+    x[2] = -0.0
+    x[3, ::7] = -0.0
+    x[3, 3::11] = rng.standard_normal((len(range(3, N, 11)), channels)) * 1e-39   # denormal samples
+    x[4, :2000] = rng.standard_normal((2000, channels)) * 1e-3
+    x[4, 30000:30050] = 1e-38
+    x[5] = rng.standard_normal((N, channels)) * 0.25
+    x[5, 20000:] = 0.0
+    y = e.process(x)
+    tiny = 0
+    for b in range(B):
+        want = CO.biquad_f32(x[b], sos)
+        tiny += int(np.count_nonzero((want != 0) & (np.abs(want) < np.finfo(np.float32).tiny)))
+        assert bits_equal(y[b], want), b
+    assert tiny > 0   # the oracle's outputs do pass through the denormal range
 
 
 def test_biquad_pointer_tables_unaligned_and_far_apart(xm, gpu):

@@ -26,7 +26,8 @@ fn = getattr(xm._lib, "xmh_dev_bq_prof", None)
 if fn is not None:
     buf = np.zeros(4096, np.uint64)
     fn(buf.ctypes.data_as(ctypes.c_void_p))
-    w = buf.reshape(2048, 2)[:(B + 11) // 12].astype(np.float64)
+    w = buf.reshape(2048, 2).astype(np.float64)
+    w = w[w[:, 0] > 0]                         # the launch's workgroups
     steps = (N + 127) // 128 + 4
     print("compute wave, cycles per 128-frame step: chunk %.0f  barrier/wait %.0f" % tuple(w.mean(0) / steps),
           flush=True)

@@ -112,48 +112,26 @@ constexpr size_t BQ_LDS = ((size_t)4 * BQ_KPW * BQ_RP + 64 * (BQ_G + 1)) * 16;  
 __device__ uint64_t g_bq_prof[4096];   // dev: per-workgroup cycles (compute wave: chunk, barrier wait)
 #endif
 
-template <int C, bool ST>
-__global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
+// The copy wave shared by both biquad kernels: every HBM access of the
+// workgroup.  inb_row(p, k) / outb_row(p, k) give the LDS granule (16 B) where
+// clip k's input / output chunk of parity p starts; chunks are 1 KB (64
+// granules) of interleaved PCM, CH frames.
+template <int C, class InRow, class OutRow>
+__device__ __forceinline__ void bq_copy_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, int ns,
+                                             InRow inb_row, OutRow outb_row)
 {
-    typedef typename BqVec<C>::T V;
     typedef const __attribute__((address_space(1))) float gcf;
     typedef __attribute__((address_space(1))) float gf;
     typedef __attribute__((address_space(1))) bq_f4u gf4u;
     typedef __attribute__((address_space(3))) void lds_void;
-    constexpr int G = BQ_G;
-    constexpr int FPL = 4 / C;                     // frames per 16-B granule
-    constexpr int CH = G * FPL;                    // frames per chunk
-    // dynamic LDS (BQ_LDS bytes), in granules:
-    //   inb rows  [parity][clip], BQ_RP apart   input chunks (DMA targets, below 64 KB)
-    //   outb rows [parity][clip], BQ_RP apart   the last sections' output chunks
-    //   sec[lane][granule], rows G + 1 apart     the other sections' output chunks
-    // sec rows land on successive 16-B bank slots (65 = 1 mod 16), so a wave's
-    // 64 reads of sec[L-1][g] (and writes of sec[L][g]) are conflict-free.  The
-    // inb / outb row of clip k is skewed to the bank slot of the sec row its
-    // lane would otherwise use (section 0 reads "row L - 1", the last section
-    // writes "row L"), which keeps the mixed accesses conflict-free too (PMC
-    // without the skew: 43 % of LDS cycles were bank conflicts).
     extern __shared__ bq_f4 bq_lds[];
-    const int ns = j.n_sos;
-    constexpr int SEC0 = 4 * BQ_KPW * BQ_RP;      // first sec row, granules (a multiple of 16)
-    bq_f4 (*sec)[G + 1] = (bq_f4 (*)[G + 1])(bq_lds + SEC0);
-    auto inb_row = [&](int p, int k) __attribute__((always_inline)) {
-        return (p * BQ_KPW + k) * BQ_RP + ((k * ns - 1) * (G + 1) & 15);
-    };
-    auto outb_row = [&](int p, int k) __attribute__((always_inline)) {
-        return ((2 + p) * BQ_KPW + k) * BQ_RP + ((k * ns + ns - 1) * (G + 1) & 15);
-    };
-    const int kpw = min(64 / ns, BQ_KPW);          // clips per workgroup
+    constexpr int FPL = 4 / C;                     // frames per 16-B granule
+    constexpr int CH = BQ_G * FPL;                 // frames per chunk
     const int lane = threadIdx.x & 63;
-    const int clip0 = blockIdx.x * kpw;
-    const int nclip = min(kpw, j.n_clips - clip0);
     const int64_t N = j.frames;
     const int64_t nchunk = (N + CH - 1) / CH;
     const int64_t nfull = N / CH;                  // chunks with no frame past N
-    const int64_t steps = nchunk + ns - 1;
-
-    if (threadIdx.x >= 64) {
-        // ---------------- copy wave: every HBM access of the workgroup ----------
+    {
         // The clip bases.  Lane k < nclip holds clip k's pointers; when the
         // clips lie within 4 GB of the lowest one (one tensor, or any compact
         // table) every access is a wave-uniform base (SGPR: the lowest pointer
@@ -264,6 +242,46 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
         }
         store_chunk(steps - ns, (int)((steps - 1) & 1));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the LDS is gone
+    }
+}
+
+template <int C, bool ST>
+__global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
+{
+    typedef typename BqVec<C>::T V;
+    constexpr int G = BQ_G;
+    constexpr int FPL = 4 / C;                     // frames per 16-B granule
+    constexpr int CH = G * FPL;                    // frames per chunk
+    // dynamic LDS (BQ_LDS bytes), in granules:
+    //   inb rows  [parity][clip], BQ_RP apart   input chunks (DMA targets, below 64 KB)
+    //   outb rows [parity][clip], BQ_RP apart   the last sections' output chunks
+    //   sec[lane][granule], rows G + 1 apart     the other sections' output chunks
+    // sec rows land on successive 16-B bank slots (65 = 1 mod 16), so a wave's
+    // 64 reads of sec[L-1][g] (and writes of sec[L][g]) are conflict-free.  The
+    // inb / outb row of clip k is skewed to the bank slot of the sec row its
+    // lane would otherwise use (section 0 reads "row L - 1", the last section
+    // writes "row L"), which keeps the mixed accesses conflict-free too (PMC
+    // without the skew: 43 % of LDS cycles were bank conflicts).
+    extern __shared__ bq_f4 bq_lds[];
+    const int ns = j.n_sos;
+    constexpr int SEC0 = 4 * BQ_KPW * BQ_RP;      // first sec row, granules (a multiple of 16)
+    bq_f4 (*sec)[G + 1] = (bq_f4 (*)[G + 1])(bq_lds + SEC0);
+    auto inb_row = [=](int p, int k) __attribute__((always_inline)) {
+        return (p * BQ_KPW + k) * BQ_RP + ((k * ns - 1) * (G + 1) & 15);
+    };
+    auto outb_row = [=](int p, int k) __attribute__((always_inline)) {
+        return ((2 + p) * BQ_KPW + k) * BQ_RP + ((k * ns + ns - 1) * (G + 1) & 15);
+    };
+    const int kpw = min(64 / ns, BQ_KPW);          // clips per workgroup
+    const int lane = threadIdx.x & 63;
+    const int clip0 = blockIdx.x * kpw;
+    const int nclip = min(kpw, j.n_clips - clip0);
+    const int64_t N = j.frames;
+    const int64_t nchunk = (N + CH - 1) / CH;
+    const int64_t steps = nchunk + ns - 1;
+
+    if (threadIdx.x >= 64) {
+        bq_copy_wave<C>(j, clip0, nclip, steps, ns, inb_row, outb_row);
         return;
     }
 
@@ -345,6 +363,254 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
     if (ST && st) {
         if constexpr (C == 2) { st[0] = z0.x; st[1] = z0.y; st[2] = z1.x; st[3] = z1.y; }
         else { st[0] = z0; st[1] = z1; }
+    }
+}
+
+// ---- one recurrence per lane: k_biquad_lane ---------------------------------
+// Lane = (clip k, section s, channel ch), scalar fp32 (no packing).  Per lane
+// and frame this is the packed kernel's 9 VALU ops, but every lane moves
+// only 4 B in and 4 B out of LDS per frame (ds_read2_b32 / ds_write2_b32 on
+// the interleaved chunk) instead of 8 + 8: the LDS store transfer (2 cycles
+// per dword, at half rate for a lone wave, MI355X_MICROARCH.md §LDS) was a
+// third of the packed compute wave's time.  Twice the waves, each ~25 %
+// faster per frame; only 1/6 of the SIMDs are busy either way.
+// Lane = 4*blk + r, blk = grp*ns + s; a group is 4/C clips (r = ci*C + ch),
+// so a workgroup holds (16 / ns) * 4 / C clips (cascades of up to 16
+// sections; longer ones take k_biquad_pipe).  Chunks, steps, the copy wave
+// and the per-step barrier are k_biquad_pipe's.
+// LDS rows (floats, BQ_LN_RS apart): inb[p][k], outb[p][k] (DMA / store
+// rows, 16-B aligned) and sec[k][s] (section s's output chunk of clip k),
+// each chunk interleaved as in HBM.  A row's base is skewed to the bank
+// slot (block & 7) * 4 (+ ci*C for sec rows) of the block that reads it, so
+// the 32 lanes of each half-wave access 32 distinct banks (sec rows are
+// written by the block before, which lands on the next slot: distinct too).
+// Lanes with no clip use the spare last row.
+//
+// MF (dev A/B only, -DXM_BQ_MF): the three feed-forward products b_r * x on
+// the matrix core, one v_mfma_f32_4x4x1_16b_f32 per frame (block lane r
+// supplies row r of A = b0, b1, b2, 0 of the block's section, every lane its
+// own x as B, D = A*B + (-0)), leaving 6 VALU ops per frame.  Measured
+// 12.1 ms vs 14.2 for k_biquad_pipe on config 4, but NOT exact: the MFMA
+// flushes denormal products and does not keep IEEE signed zeros
+// (tools/ubench/bq_mfma.hip: 1948 value and 45866 zero-sign mismatches in
+// 16.8M products), so silence and decaying tails would differ from sosfilt.
+constexpr int BQ_LN_RS = 288;                      // floats per row: 256 + 32 of skew
+constexpr int BQ_LN_ROWS = 128;                    // 2 x 16 inb + 2 x 16 outb + 64 sec
+static_assert((size_t)BQ_LN_RS * BQ_LN_ROWS * 4 <= BQ_LDS, "rows fit the launch's LDS");
+
+// two frames (a, b) of one chain, products on the VALU, in bq_step2's order
+// (each dependent op one instruction behind its producer)
+__device__ __forceinline__ __attribute__((unused)) void bq_lane_pair(float xa, float xb, float &z0, float &z1, float b0, float b1, float b2,
+                                             float na1, float na2, float &oa, float &ob)
+{
+    float p0, p1, p2, t, u;
+    asm volatile(
+        "v_mul_f32 %[p0], %[b0], %[xa]\n\t"
+        "v_mul_f32 %[p1], %[b1], %[xa]\n\t"
+        "v_add_f32 %[oa], %[z0], %[p0]\n\t"
+        "v_mul_f32 %[p2], %[b2], %[xa]\n\t"
+        "v_mul_f32 %[t], %[na1], %[oa]\n\t"
+        "v_mul_f32 %[p0], %[b0], %[xb]\n\t"
+        "v_add_f32 %[t], %[p1], %[t]\n\t"
+        "v_mul_f32 %[u], %[na2], %[oa]\n\t"
+        "v_add_f32 %[z0], %[z1], %[t]\n\t"
+        "v_add_f32 %[z1], %[p2], %[u]\n\t"
+        "v_add_f32 %[ob], %[z0], %[p0]\n\t"
+        "v_mul_f32 %[p1], %[b1], %[xb]\n\t"
+        "v_mul_f32 %[t], %[na1], %[ob]\n\t"
+        "v_mul_f32 %[p2], %[b2], %[xb]\n\t"
+        "v_add_f32 %[t], %[p1], %[t]\n\t"
+        "v_mul_f32 %[u], %[na2], %[ob]\n\t"
+        "v_add_f32 %[z0], %[z1], %[t]\n\t"
+        "v_add_f32 %[z1], %[p2], %[u]"
+        : [oa] "=&v"(oa), [ob] "=&v"(ob), [p0] "=&v"(p0), [p1] "=&v"(p1), [p2] "=&v"(p2), [t] "=&v"(t),
+          [u] "=&v"(u), [z0] "+v"(z0), [z1] "+v"(z1)
+        : [xa] "v"(xa), [xb] "v"(xb), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [na1] "v"(na1), [na2] "v"(na2));
+}
+
+// MF: two frames from precomputed products (z1 alternates with w: no move)
+__device__ __forceinline__ __attribute__((unused)) void bq_mf_pair(const float (&pa)[4], const float (&pb)[4], float &z0, float &z1, float na1,
+                                           float na2, float &oa, float &ob)
+{
+    float t, u, w;
+    asm volatile(
+        "v_add_f32 %[oa], %[z0], %[pa0]\n\t"
+        "v_mul_f32 %[t], %[na1], %[oa]\n\t"
+        "v_mul_f32 %[u], %[na2], %[oa]\n\t"
+        "v_add_f32 %[t], %[pa1], %[t]\n\t"
+        "v_add_f32 %[w], %[pa2], %[u]\n\t"
+        "v_add_f32 %[z0], %[z1], %[t]\n\t"
+        "v_add_f32 %[ob], %[z0], %[pb0]\n\t"
+        "v_mul_f32 %[t], %[na1], %[ob]\n\t"
+        "v_mul_f32 %[u], %[na2], %[ob]\n\t"
+        "v_add_f32 %[t], %[pb1], %[t]\n\t"
+        "v_add_f32 %[z1], %[pb2], %[u]\n\t"
+        "v_add_f32 %[z0], %[w], %[t]"
+        : [oa] "=&v"(oa), [ob] "=&v"(ob), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w), [z0] "+v"(z0), [z1] "+v"(z1)
+        : [pa0] "v"(pa[0]), [pa1] "v"(pa[1]), [pa2] "v"(pa[2]), [pb0] "v"(pb[0]), [pb1] "v"(pb[1]), [pb2] "v"(pb[2]),
+          [na1] "v"(na1), [na2] "v"(na2));
+}
+
+template <int C, bool ST, bool MF = false>
+__global__ __launch_bounds__(128) void k_biquad_lane(XmhFxJob j)
+{
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    constexpr int FPL = 4 / C;
+    constexpr int CH = BQ_G * FPL;                 // frames per chunk
+    constexpr int NQ = CH / 4;                     // quads (4 frames of one channel) per chunk
+    constexpr int CPG = 4 / C;                     // clips per group
+    extern __shared__ bq_f4 bq_lds[];
+    float *lf = (float *)bq_lds;
+    const int ns = j.n_sos;
+    const int gpw = 16 / ns;                       // groups per wave
+    const int kpw = min(gpw * CPG, BQ_KPW);        // clips per workgroup
+    const int clip0 = blockIdx.x * kpw;
+    const int nclip = min(kpw, j.n_clips - clip0);
+    const int64_t N = j.frames;
+    const int64_t nchunk = (N + CH - 1) / CH;
+    const int64_t steps = nchunk + ns - 1;
+    // row bases (floats); the slot of clip k's section-s block is ((k / CPG) * ns + s) & 7
+    auto slot = [=](int k, int s) __attribute__((always_inline)) { return (((k / CPG) * ns + s) & 7) * 4; };
+    auto inb_f = [=](int p, int k) __attribute__((always_inline)) { return (p * 16 + k) * BQ_LN_RS + slot(k, 0); };
+    auto outb_f = [=](int p, int k) __attribute__((always_inline)) {
+        return (32 + p * 16 + k) * BQ_LN_RS + slot(k, ns);
+    };
+    auto sec_f = [=](int k, int s) __attribute__((always_inline)) {   // read by section s + 1
+        return (64 + k * ns + s) * BQ_LN_RS + slot(k, s + 1) + (k % CPG) * C;
+    };
+
+    if (threadIdx.x >= 64) {
+        bq_copy_wave<C>(j, clip0, nclip, steps, ns, [=](int p, int k) { return inb_f(p, k) / 4; },
+                        [=](int p, int k) { return outb_f(p, k) / 4; });
+        return;
+    }
+
+    const int lane = threadIdx.x & 63;
+    const int blk = lane >> 2, r = lane & 3;
+    const int grp = blk / ns, s = blk % ns, ci = r / C, ch = r % C;
+    const int kk = grp * CPG + ci;
+    const bool valid = blk < gpw * ns && kk < nclip;
+    const float *q = j.sos + 6 * s;
+    const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
+    const float na1 = -a1, na2 = -a2;              // (-a)*o == -(a*o): IEEE negation is exact
+    [[maybe_unused]] const float A = r < 3 ? q[r] : 0.0f;   // MF: row r of the block's A
+    float z0 = 0.0f, z1 = 0.0f;
+    float *st = (ST && valid) ? j.state + ((size_t)(clip0 + kk) * ns + s) * 2 * C : nullptr;
+    if (ST && st) {
+        z0 = st[ch];
+        z1 = st[C + ch];
+    }
+    const bool last = s == ns - 1;
+    const int spare = (BQ_LN_ROWS - 1) * BQ_LN_RS + (lane & 31) - ch;   // + ch below: within the row
+    const int src_sec = valid ? (s ? sec_f(kk, s - 1) : -1) : spare;
+    const int dst_row = valid ? (last ? -1 : sec_f(kk, s)) : spare;
+#ifdef XM_BQ_PROF
+    uint64_t pr[2] = {0, 0}, tq = __builtin_amdgcn_s_memtime();
+#define XM_BQ_T(n) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pr[n] += t_ - tq; tq = t_; } while (0)
+#else
+#define XM_BQ_T(n) do { } while (0)
+#endif
+    __syncthreads();
+    for (int64_t i = 0; i < steps; ++i) {
+        XM_BQ_T(1);
+        const int64_t c = i - s;                   // chunk this lane filters
+        // every lane runs the chunk (uniform control flow); a lane outside its
+        // chunk range keeps its state and its outputs are never used
+        const bool act = valid && c >= 0 && c < nchunk;
+        const float z0s = z0, z1s = z1;
+        const int par = (int)(i & 1);
+        const float *src = lf + (src_sec >= 0 ? src_sec : inb_f(par, kk)) + ch;
+        float *dst = lf + (dst_row >= 0 ? dst_row : outb_f(par, kk)) + ch;
+        const bool tail = ST && st && act && (c + 1) * CH > N;
+        if (__builtin_amdgcn_ballot_w64(tail) != 0) {
+            // a streamed block's last chunk: frames past N are padding and must
+            // not advance the state (wave-uniform branch)
+            for (int f = 0; f < CH; ++f) {
+                const float v = src[f * C];
+                const float o = b0 * v + z0;
+                if (!(tail && c * CH + f >= N)) {
+                    z0 = (b1 * v - a1 * o) + z1;
+                    z1 = b2 * v - a2 * o;
+                }
+                dst[f * C] = o;
+            }
+        } else if constexpr (!MF) {
+            // quads: x of quad qd + 2 is read while quad qd is filtered (before
+            // the left neighbour's writes of this step reach it)
+            float xa[4], xb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xa[e] = src[e * C];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xb[e] = src[(4 + e) * C];
+#pragma unroll
+            for (int qd = 0; qd < NQ; ++qd) {
+                float xn[4];
+                if (qd + 2 < NQ) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) xn[e] = src[(4 * (qd + 2) + e) * C];
+                }
+                float o[4];
+                bq_lane_pair(xa[0], xa[1], z0, z1, b0, b1, b2, na1, na2, o[0], o[1]);
+                bq_lane_pair(xa[2], xa[3], z0, z1, b0, b1, b2, na1, na2, o[2], o[3]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dst[(4 * qd + e) * C] = o[e];
+                asm volatile("" ::: "memory");     // later quads' reads stay behind these writes
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    xa[e] = xb[e];
+                    if (qd + 2 < NQ) xb[e] = xn[e];
+                }
+            }
+        } else {
+            const f4v nz = {-0.0f, -0.0f, -0.0f, -0.0f};
+            float xb[4];
+            float P[2][4][4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const f4v d = __builtin_amdgcn_mfma_f32_4x4x1f32(A, src[e * C], nz, 0, 0, 0);
+                P[0][e][0] = d[0]; P[0][e][1] = d[1]; P[0][e][2] = d[2];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xb[e] = src[(4 + e) * C];
+#pragma unroll
+            for (int qd = 0; qd < NQ; ++qd) {
+                const int cb = qd & 1;
+                float xn[4];
+                if (qd + 2 < NQ) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) xn[e] = src[(4 * (qd + 2) + e) * C];
+                }
+                if (qd + 1 < NQ) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const f4v d = __builtin_amdgcn_mfma_f32_4x4x1f32(A, xb[e], nz, 0, 0, 0);
+                        P[cb ^ 1][e][0] = d[0]; P[cb ^ 1][e][1] = d[1]; P[cb ^ 1][e][2] = d[2];
+                    }
+                }
+                float o[4];
+                bq_mf_pair(P[cb][0], P[cb][1], z0, z1, na1, na2, o[0], o[1]);
+                bq_mf_pair(P[cb][2], P[cb][3], z0, z1, na1, na2, o[2], o[3]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dst[(4 * qd + e) * C] = o[e];
+                asm volatile("" ::: "memory");
+                if (qd + 2 < NQ) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) xb[e] = xn[e];
+                }
+            }
+        }
+        if (!act) { z0 = z0s; z1 = z1s; }
+        XM_BQ_T(0);
+        __syncthreads();                           // chunk i + 1 staged; outputs visible to the copy wave
+    }
+#ifdef XM_BQ_PROF
+    if (lane == 0 && blockIdx.x < 2048)
+        for (int n = 0; n < 2; ++n) g_bq_prof[blockIdx.x * 2 + n] = pr[n];
+#endif
+#undef XM_BQ_T
+    if (ST && st) {
+        st[ch] = z0;
+        st[C + ch] = z1;
     }
 }
 
@@ -444,12 +710,27 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
     if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
     if (j->n_clips == 0 || j->frames == 0) return 0;
 
-    auto kern = j->channels == 2 ? (j->state ? k_biquad_pipe<2, true> : k_biquad_pipe<2, false>)
-                                 : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>);
-    const int kpw = std::min(64 / j->n_sos, BQ_KPW);
+    // cascades of up to 16 sections: one recurrence per lane (k_biquad_lane);
+    // longer ones: the packed kernel.  Dev A/B builds: -DXM_BQ_PACKED_ONLY,
+    // -DXM_BQ_MF (matrix-core products: not exact, see k_biquad_lane)
+#ifdef XM_BQ_PACKED_ONLY
+    const bool mf = false;
+#else
+    const bool mf = j->n_sos <= 16;
+#endif
+#ifdef XM_BQ_MF
+    constexpr bool MFP = true;
+#else
+    constexpr bool MFP = false;
+#endif
+    auto kern = mf ? (j->channels == 2 ? (j->state ? k_biquad_lane<2, true, MFP> : k_biquad_lane<2, false, MFP>)
+                                       : (j->state ? k_biquad_lane<1, true, MFP> : k_biquad_lane<1, false, MFP>))
+                   : (j->channels == 2 ? (j->state ? k_biquad_pipe<2, true> : k_biquad_pipe<2, false>)
+                                       : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>));
+    const int kpw = mf ? std::min(16 / j->n_sos * (4 / j->channels), BQ_KPW) : std::min(64 / j->n_sos, BQ_KPW);
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    static std::atomic<int> lds_set[4];            // per (C, ST) instantiation, set once per process
-    const int ki = (j->channels == 2) * 2 + (j->state != nullptr);
+    static std::atomic<int> lds_set[8];            // per (kernel, C, ST) instantiation, set once per process
+    const int ki = mf * 4 + (j->channels == 2) * 2 + (j->state != nullptr);
     if (!lds_set[ki].load(std::memory_order_acquire)) {
         if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BQ_LDS) !=
             hipSuccess)
