@@ -18,7 +18,8 @@ up      44.1k -> 48k fp32 (generic kernel)
 s16rs   48k -> 44.1k s16 Q15 (generic kernel)
 planar  48k -> 44.1k fp32, planar tracks and mixes (generic kernel)
 conv    48k -> 44.1k, s16 tracks into the fp32 mix (generic kernel)
-stream  the headline pushed in 8 blocks through stream_push (generic kernel)
+stream  the headline pushed in 8 blocks through stream_push (fused bulk + generic heads)
+oconv   the headline with XM_MIXER_OUT_CONVERT: s16 output (fused kernel epilogue)
 Unit: input samples (frames x channels x tracks) per second; roofline
 fraction = algorithmic bytes (inputs once + output once) / kernel time / 8 TB/s.
 Inputs are synthetic PCM generated in HBM (xm_synth_pcm), outside the timing.
@@ -148,16 +149,17 @@ def c5(a):
 
 
 def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=False, conv=False,
-           stream=False):
+           stream=False, oconv=False):
     B, ntr = a.mixes, 8
-    m = xm.Mixer(fi, fo, 2, fmt, mem="device", planar=planar, convert_in=conv)
+    m = xm.Mixer(fi, fo, 2, fmt, mem="device", planar=planar, convert_in=conv, convert_out=oconv)
     m.set_tracks(Q15_RAMPS if fmt == "s16" else RAMPS)
     F = m.out_frames(N)
     ifmt = "s16" if (fmt == "s16") != conv else "f32"
     isz = 2 if ifmt == "s16" else 4
-    osz = 2 if fmt == "s16" else 4
+    ofmt = "s16" if (fmt == "s16") != oconv else "f32"
+    osz = 2 if ofmt == "s16" else 4
     x = torch.empty((B, ntr, N, 2), dtype=torch.int16 if ifmt == "s16" else torch.float32, device="cuda")
-    y = torch.empty((B, F, 2), dtype=torch.int16 if fmt == "s16" else torch.float32, device="cuda")
+    y = torch.empty((B, F, 2), dtype=torch.int16 if ofmt == "s16" else torch.float32, device="cuda")
     s = torch.cuda.current_stream()
     xm.synth(x.data_ptr(), ifmt, SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
     m.set_stream(s.cuda_stream)
@@ -184,7 +186,8 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
         step = lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)  # noqa: E731
     w, k = timed(step, a.steps, a.warmup, s)
     fast = m.timing().fast_launches
-    report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix",
+    report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix"
+           + (f", {ofmt} out" if oconv else ""),
            B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m,
            kernel="k_rs147_mix" if fast else "generic")
 
@@ -196,6 +199,7 @@ def s16rs(a): _shape(a, "s16rs", fmt="s16")
 def planar(a): _shape(a, "planar", planar=True)
 def conv(a): _shape(a, "conv", conv=True)
 def stream(a): _shape(a, "stream", stream=True)
+def oconv(a): _shape(a, "oconv", oconv=True)
 
 
 def main():

@@ -827,7 +827,7 @@ size_t xm_audio_mixer_stream_out_frames(const XmAudioMixer *m, size_t frames_in,
 static int st_fast_part(XmAudioMixer *m, XmhMixJob *j, int64_t R, const char *win, size_t fb, int *launches)
 {
     const int64_t L = m->table.d.L, M = m->table.d.M;
-    if (L != 147 || M != 160 || !m->table.fast || j->io_flags || j->out_conv) return XM_OK;
+    if (L != 147 || M != 160 || !m->table.fast || j->io_flags) return XM_OK;   /* out_conv 1: the kernel's s16 epilogue */
     const int64_t ob = j->out_base, oe = ob + j->frames_out;
     const int64_t ob_al = (ob + L - 1) / L * L, a0 = ob_al / L * M;
     if (oe - ob_al < 4 * L || a0 >= R || (a0 > 0 && a0 - 32 < m->st_w0)) return XM_OK;   /* too small to pay */
