@@ -80,3 +80,62 @@ def test_fast_stream_convert_out(xm, gpu):
     assert bits_equal(ys, whole)
     ref, _ = CO.batch_resample_mix_f32(x, RAMPS, 147, 160, threads=2)
     assert bits_equal(whole, _to_s16(ref))
+
+
+@pytest.mark.parametrize("N", [48000, 48001, 48002, 48003, 160 * 40 + 33])
+@pytest.mark.parametrize("convert_out", [False, True])
+def test_fast_s16_tracks_into_f32_mix(xm, gpu, N, convert_out):
+    """XM_MIXER_IN_CONVERT on the fused kernel: 8 s16 tracks (4-B frames,
+    128-B DMA segments) read as x * 2^-15 into the f32 mix; every N mod 4
+    (a partial last 4-frame chunk holds the next track's first samples,
+    which the copy zeroes), full-scale samples, optionally s16 out."""
+    from bench import RAMPS
+    B = 3
+    x = np.stack([np.stack([O.gen_s16(SEED, 6200 + 8 * b + t, 2, N) for t in range(8)]) for b in range(B)])
+    x[:, :, 300:340] = 32767
+    x[:, 3:, 700:720] = -32768
+    m = xm.Mixer(48000, 44100, 2, "f32", convert_in=True, convert_out=convert_out)
+    m.set_tracks(RAMPS)
+    y = m.process(x)
+    t = m.timing()
+    assert t.fast_launches == 1, (t.n_launches, t.fast_launches)
+    xf = x.astype(np.float32) * np.float32(2.0 ** -15)
+    ref, _ = CO.batch_resample_mix_f32(xf, RAMPS, 147, 160, threads=2)
+    assert bits_equal(y, _to_s16(ref) if convert_out else ref)
+
+
+def test_fast_s16_in_device_strides_and_tables(xm, gpu):
+    """Device memory, s16 tracks at padded strides (frames 4-B aligned, not
+    16-B) and through a scattered pointer table: the same bits as the
+    oracle, on the fused kernel."""
+    import torch
+    from bench import RAMPS
+    N, B, ntr = 9601, 3, 8
+    x = np.stack([np.stack([O.gen_s16(SEED, 6300 + 8 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    ts, ms = N * 2 + 6, (N * 2 + 6) * ntr + 10
+    buf = np.zeros(B * ms, np.int16)
+    for b in range(B):
+        for t in range(ntr):
+            buf[b * ms + t * ts: b * ms + t * ts + 2 * N] = x[b, t].reshape(-1)
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device", convert_in=True)
+    m.set_tracks(RAMPS)
+    F = m.out_frames(N)
+    xd = torch.from_numpy(buf).cuda()
+    yd = torch.zeros((B, F * 2 + 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    m.process_strided(xd.data_ptr(), ts, ms, yd.data_ptr(), F * 2 + 4, B, N)
+    torch.cuda.synchronize()
+    assert m.timing().fast_launches == 1
+    xf = x.astype(np.float32) * np.float32(2.0 ** -15)
+    ref, _ = CO.batch_resample_mix_f32(xf, RAMPS, 147, 160, threads=2)
+    y = yd.cpu().numpy()[:, :2 * F].reshape(B, F, 2)
+    assert bits_equal(y, ref)
+    # pointer table: every mix's tracks in a scattered order inside the buffer
+    perm = [(3 * t + 5) % ntr for t in range(ntr)]
+    ins = [xd[b * ms + perm[t] * ts:].data_ptr() for b in range(B) for t in range(ntr)]
+    y2 = torch.zeros((B, F, 2), dtype=torch.float32, device="cuda")
+    m.process_ptrs(ins, [y2[b].data_ptr() for b in range(B)], B, N)
+    torch.cuda.synchronize()
+    assert m.timing().fast_launches == 1
+    ref2, _ = CO.batch_resample_mix_f32(xf[:, perm], RAMPS, 147, 160, threads=2)
+    assert bits_equal(y2.cpu().numpy(), ref2)
