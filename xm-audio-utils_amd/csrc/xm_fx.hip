@@ -4,8 +4,10 @@
 // Biquad: scipy sosfilt order (transposed DF-II, _signaltools.py:4601),
 // sections in order, state zero at clip start.  The recurrence is serial in
 // time, so exactness (SURVEY.md §7 hard part 3) limits the parallelism to
-// clips x sections: k_biquad_pipe gives each (clip, section) its own lane
-// and chains the sections through LDS (see the comment at the kernel).
+// clips x sections x channels: k_biquad_lane (cascades of up to 16
+// sections) gives each (clip, section, channel) its own lane, k_biquad_pipe
+// (longer cascades) each (clip, section) with stereo packed; both chain the
+// sections through LDS (see the comments at the kernels).
 // FIR: upfirdn order (_upfirdn.py:107), taps staged in LDS, input tile in LDS.
 #include <stdlib.h>
 #include <algorithm>
