@@ -139,3 +139,53 @@ def test_fast_s16_in_device_strides_and_tables(xm, gpu):
     assert m.timing().fast_launches == 1
     ref2, _ = CO.batch_resample_mix_f32(xf[:, perm], RAMPS, 147, 160, threads=2)
     assert bits_equal(y2.cpu().numpy(), ref2)
+
+
+Q15_RAMPS = [dict(gain0_q15=29491), dict(gain0_q15=0, gain1_q15=26214, ramp_start=0, ramp_len=4800),
+             dict(gain0_q15=22938, gain1_q15=6554, ramp_start=2400, ramp_len=9600), dict(gain0_q15=65535),
+             dict(mode=1, ramp_start=1440, ramp_len=9601),
+             dict(gain0_q15=0, gain1_q15=32768, ramp_start=14400, ramp_len=9599),
+             dict(gain0_q15=32768, gain1_q15=0, ramp_start=43200, ramp_len=4800),
+             dict(gain0_q15=9830, gain1_q15=19661, ramp_start=30000, ramp_len=0)]
+
+
+@pytest.mark.parametrize("N", [48000, 48003, 160 * 40 + 33])
+@pytest.mark.parametrize("convert_out", [False, True])
+def test_fast_s16_q15_mix(xm, gpu, N, convert_out):
+    """s16 tracks into the s16 Q15 mix on the fused kernel: each track
+    resampled in fp32 on its integer samples, sat16(rint(r)), times its Q15
+    ramp (rising, falling, crossfade-out, step, gain 65535: the ramps' integer
+    quotients advance per output without a division), (s*g + 2^14) >> 15,
+    int32 sum, sat16; optionally f32 out (sat16 * 2^-15)."""
+    B = 3
+    x = np.stack([np.stack([O.gen_s16(SEED, 6400 + 8 * b + t, 2, N) for t in range(8)]) for b in range(B)])
+    x[:, :, 300:340] = 32767             # full scale: every saturation stage
+    x[:, 3:, 700:720] = -32768
+    m = xm.Mixer(48000, 44100, 2, "s16", convert_out=convert_out)
+    m.set_tracks(Q15_RAMPS)
+    y = m.process(x)
+    t = m.timing()
+    assert t.fast_launches == 1, (t.n_launches, t.fast_launches)
+    for b in range(B):
+        ref = CO.resample_mix_s16(list(x[b]), Q15_RAMPS, 147, 160)
+        if convert_out:
+            ref = ref.astype(np.float32) * np.float32(2.0 ** -15)
+        assert bits_equal(y[b], ref), b
+
+
+def test_fast_s16_q15_long_ramps(xm, gpu):
+    """Ramps of hundreds of thousands of frames: (q1 - q0) * k passes 2^31,
+    so the per-SP start of the incremental quotient needs its 64-bit form;
+    rising, falling and crossfade-out ramps, 10 s clips."""
+    N, B = 480000, 2
+    ramps = [dict(gain0_q15=0, gain1_q15=65535, ramp_start=1000, ramp_len=400000),
+             dict(gain0_q15=60000, gain1_q15=100, ramp_start=0, ramp_len=441000),
+             dict(mode=1, ramp_start=5000, ramp_len=300001),
+             dict(gain0_q15=32768, gain1_q15=1, ramp_start=200000, ramp_len=240000)] * 2
+    x = np.stack([np.stack([O.gen_s16(SEED, 6500 + 8 * b + t, 2, N) for t in range(8)]) for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "s16")
+    m.set_tracks(ramps)
+    y = m.process(x)
+    assert m.timing().fast_launches == 1
+    for b in range(B):
+        assert bits_equal(y[b], CO.resample_mix_s16(list(x[b]), ramps, 147, 160)), b
