@@ -189,3 +189,46 @@ def test_fast_s16_q15_long_ramps(xm, gpu):
     assert m.timing().fast_launches == 1
     for b in range(B):
         assert bits_equal(y[b], CO.resample_mix_s16(list(x[b]), ramps, 147, 160)), b
+
+
+def _planar(a):
+    """[..., frames, channels] -> [..., channels, frames]"""
+    return np.ascontiguousarray(np.swapaxes(a, -1, -2))
+
+
+@pytest.mark.parametrize("N", [48000, 48001, 48003, 160 * 40 + 33])
+def test_fast_planar_mix(xm, gpu, N):
+    """XM_MIXER_PLANAR on the fused kernel: planar f32 tracks (plane R at
+    +N samples, so for N mod 4 != 0 a partial chunk of plane L holds plane
+    R's first samples, zeroed on the copy) and planar mixes (two b32 stores
+    per output)."""
+    from bench import RAMPS
+    B = 3
+    x = np.stack([np.stack([O.gen_f32(SEED, 6600 + 8 * b + t, 2, N) for t in range(8)]) for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "f32", planar=True)
+    m.set_tracks(RAMPS)
+    y = m.process(_planar(x))
+    assert m.timing().fast_launches == 1
+    ref, _ = CO.batch_resample_mix_f32(x, RAMPS, 147, 160, threads=2)
+    assert bits_equal(y, _planar(ref))
+
+
+def test_fast_planar_device_pointer_table(xm, gpu):
+    """Planar tracks through a scattered pointer table in device memory."""
+    import torch
+    from bench import RAMPS
+    N, B = 9601, 2
+    x = np.stack([np.stack([O.gen_f32(SEED, 6700 + 8 * b + t, 2, N) for t in range(8)]) for b in range(B)])
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device", planar=True)
+    m.set_tracks(RAMPS)
+    F = m.out_frames(N)
+    xd = torch.from_numpy(_planar(x)).cuda()               # [B][8][2][N]
+    perm = [(5 * t + 1) % 8 for t in range(8)]
+    ins = [xd[b, perm[t]].data_ptr() for b in range(B) for t in range(8)]
+    y = torch.full((B, 2, F), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    m.process_ptrs(ins, [y[b].data_ptr() for b in range(B)], B, N)
+    torch.cuda.synchronize()
+    assert m.timing().fast_launches == 1
+    ref, _ = CO.batch_resample_mix_f32(x[:, perm], RAMPS, 147, 160, threads=2)
+    assert bits_equal(y.cpu().numpy(), _planar(ref))

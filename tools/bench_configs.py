@@ -15,9 +15,9 @@ ramps, the kernel each one lands on in "kernel"):
 odd     frames_in 480001 (fused kernel, odd-length path)
 ptrs    irregular pointer table (tracks in scattered order: generic kernel)
 up      44.1k -> 48k fp32 (generic kernel)
-s16rs   48k -> 44.1k s16 Q15 (generic kernel)
-planar  48k -> 44.1k fp32, planar tracks and mixes (generic kernel)
-conv    48k -> 44.1k, s16 tracks into the fp32 mix (generic kernel)
+s16rs   48k -> 44.1k s16 Q15 (fused kernel, IO 2)
+planar  48k -> 44.1k fp32, planar tracks and mixes (fused kernel, PL)
+conv    48k -> 44.1k, s16 tracks into the fp32 mix (fused kernel, IO 1)
 stream  the headline pushed in 8 blocks through stream_push (fused bulk + generic heads)
 oconv   the headline with XM_MIXER_OUT_CONVERT: s16 output (fused kernel epilogue)
 Unit: input samples (frames x channels x tracks) per second; roofline
