@@ -121,7 +121,11 @@ XM_API int xm_audio_mixer_set_crossfade(XmAudioMixer *m, int track_from, int tra
                                  int64_t start, int64_t len);
 
 /* Attach an effects chain applied to every track after resampling and before
- * the gain (NULL detaches).  The chain's rate/channels must match the mix. */
+ * the gain (NULL detaches).  The chain's rate/channels must match the mix.
+ * A single-device handle keeps the pointer and reads the chain at each call
+ * (the chain must live on the handle's device).  A multi-device handle copies
+ * the chain onto each of its devices here, so effects added to `fx` later do
+ * not reach it until set_track_effects is called again. */
 XM_API int xm_audio_mixer_set_track_effects(XmAudioMixer *m, const struct XmEffects *fx);
 
 /* Output frames per mix for a given input length. */

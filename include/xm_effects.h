@@ -41,8 +41,27 @@ typedef struct XmEffectsConfig {
 } XmEffectsConfig;
 
 XM_API XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status);
-/* Host-memory chain on device 0 (SURVEY.md §8(b) form; n_devices must be 1). */
+/* Host-memory chain (SURVEY.md §8(b) form): n_devices == 1 on device 0,
+ * n_devices > 1 over devices 0 .. n_devices-1 (xm_effects_create_multi);
+ * NULL if n_devices is out of [1, 16] or names a device that is not there. */
 XM_API XmEffects *xm_effects_create(int rate, int channels, int n_devices);
+
+/* Multi-device chain over an explicit device list (n_devices in [1, 16]; a
+ * device may repeat).  One single-device chain and one host worker thread per
+ * entry ("one host worker thread per GPU, joined before
+ * process_batch returns").  Effects added to the handle reach every device.
+ * process_batch / process_stream cut the clips into contiguous blocks, block
+ * d (the first batch % n blocks one clip longer) on device d, and return when
+ * every device is done; clips are independent, so the result equals the
+ * one-device result bit for bit.  With XM_MEM_DEVICE, block d's pointers must
+ * be on device d.  cfg->device is ignored; set_stream returns XM_ENOSYS.
+ * Such a chain attaches to multi-device mixers (copied per device), not to a
+ * single-device mixer (XM_EINVAL there). */
+XM_API XmEffects *xm_effects_create_multi(const XmEffectsConfig *cfg, const int *devices, int n_devices,
+                                          int *status);
+
+/* Devices a chain runs on (1 for a single-device chain). */
+XM_API int xm_effects_n_devices(const XmEffects *e);
 
 /* sos = {b0, b1, b2, a0, a1, a2}; a0 must be 1 (as scipy sosfilt requires).
  * A chain holds up to 128 effects (XM_ENOMEM beyond); consecutive biquads run

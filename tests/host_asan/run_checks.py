@@ -169,6 +169,63 @@ def main():
         o3 = mm.stream_flush()
         check(f"multi-device {devs} streaming",
               beq(np.concatenate([o1, o2, o3], axis=1), CO.batch_resample_mix_f32(x5, RAMPS, 147, 160)[0]))
+    # a track list that fails on device 1 leaves the multi-device handle with
+    # its previous list on every device (single-device rule)
+    import ctypes
+    mm = xm.Mixer(48000, 44100, 2, "f32", devices=[0, 1])
+    mm.set_tracks(RAMPS)
+    x5 = f32_tracks(3, 8, 500, base=260)
+    xm._lib.xm_fake_fail_device.argtypes = [ctypes.c_int]
+    xm._lib.xm_fake_fail_device(1)
+    try:
+        mm.set_tracks(RAMPS[:7] + [dict(in_rate=22050)])   # sub 1 must design a table: fails there
+        failed = False
+    except xm.XmError as ex:
+        failed = ex.code == xm.XM_EDEVICE
+    xm._lib.xm_fake_fail_device(-1)
+    mm.n_tracks = 8
+    check("multi-device set_tracks failure keeps the old list",
+          failed and beq(mm.process(x5), CO.batch_resample_mix_f32(x5, RAMPS, 147, 160)[0]))
+
+    # multi-device effects chains: effects added after creation reach every
+    # device; batches and streams split over the devices
+    for devs in ([0, 1], [0, 0, 1]):
+        me = xm.Effects(44100, 2, devices=devs)
+        for sv in sos:
+            me.add_biquad(sv)
+        me.add_fir(h)
+        xe7 = f32_tracks(7, 1, 555, base=400)[:, 0]
+        re7 = np.stack([CO.fir_f32(CO.biquad_f32(xe7[b], sos), h) for b in range(7)])
+        check(f"multi-device effects {devs} batch", me.n_devices() == len(devs) and beq(me.process(xe7), re7))
+        me.stream_reset(7)
+        yst7 = np.concatenate([me.process_stream(xe7[:, :100]), me.process_stream(xe7[:, 100:101]),
+                               me.process_stream(xe7[:, 101:])], axis=1)
+        check(f"multi-device effects {devs} streaming", beq(yst7, re7))
+        try:
+            me.set_stream(None)
+            ok = False
+        except xm.XmError as ex:
+            ok = ex.code == xm.XM_ENOSYS
+        check(f"multi-device effects {devs} set_stream refused", ok)
+        mm2 = xm.Mixer(48000, 44100, 2, "f32", devices=[0, 1])
+        mm2.set_tracks(RAMPS)
+        mm2.set_track_effects(me)
+        check(f"multi-device mixer with multi-device effects {devs}",
+              beq(mm2.process(x5), np.stack([CO.mix_f32([CO.fir_f32(CO.biquad_f32(
+                  CO.resample_f32(x5[b, t], 147, 160), sos), h) for t in range(8)], RAMPS) for b in range(3)])))
+        single = xm.Mixer(48000, 44100, 2, "f32")
+        try:
+            single.set_track_effects(me)
+            ok = False
+        except xm.XmError as ex:
+            ok = ex.code == xm.XM_EINVAL
+        check(f"single-device mixer refuses a multi-device chain {devs}", ok)
+    xm._lib.xm_effects_create.restype = ctypes.c_void_p
+    hc = xm._lib.xm_effects_create(44100, 2, 2)
+    hz = xm._lib.xm_effects_create(44100, 2, 3)     # only 2 fake devices
+    check("xm_effects_create(n_devices=2) / (3 -> NULL)", bool(hc) and not hz and xm._lib.xm_effects_n_devices(hc) == 2)
+    xm._lib.xm_effects_freep(ctypes.byref(ctypes.c_void_p(hc)))
+
     q64 = s16_tracks(4, 64, 240, base=300)
     ramps64 = (Q15 * 8)[:64]
     want64 = CO.batch_mix_s16(q64, ramps64)[0]

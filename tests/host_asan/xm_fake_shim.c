@@ -30,8 +30,12 @@ static int fake_devices(void)
     return e ? atoi(e) : 1;
 }
 
+/* failure injection for the checks: xmh_set_device(dev) fails while dev == fail_dev */
+static int fail_dev = -1;
+__attribute__((visibility("default"))) void xm_fake_fail_device(int dev) { fail_dev = dev; }
+
 int xmh_device_count(void) { return fake_devices(); }
-int xmh_set_device(int dev) { return dev >= 0 && dev < fake_devices() ? 0 : -1001; }
+int xmh_set_device(int dev) { return dev >= 0 && dev < fake_devices() && dev != fail_dev ? 0 : -1001; }
 
 int xmh_malloc(void **p, size_t bytes)
 {

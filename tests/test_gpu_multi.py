@@ -174,7 +174,55 @@ def test_mix_spanning_in_library(xm, gpu, devices, rate_out):
     m.mix_spanning_s16([t.data_ptr() for t in xs], N * 2, per * N * 2, [t.data_ptr() for t in ys], F * 2, B, N)
     got = np.concatenate([t.cpu().numpy() for t in ys])
     assert bits_equal(got, want)
-    # the same handle then runs ordinary full-list calls again
+    # the same handle then runs ordinary full-list calls again (its subs go
+    # back from their config-5 subsets to the full 64-track list)
+    xall = torch.from_numpy(x).cuda()
+    yall = torch.zeros((B, F, 2), dtype=torch.int16, device="cuda")
+    ins = [xall[b, t].data_ptr() for b in range(B) for t in range(64)]
+    m.process_ptrs(ins, [yall[b].data_ptr() for b in range(B)], B, N)
+    assert bits_equal(yall.cpu().numpy(), want)
+    # and config 5 once more on the same handle
+    for t in ys:
+        t.zero_()
+    m.mix_spanning_s16([t.data_ptr() for t in xs], N * 2, per * N * 2, [t.data_ptr() for t in ys], F * 2, B, N)
+    assert bits_equal(np.concatenate([t.cpu().numpy() for t in ys]), want)
     h = xm.Mixer(48000, rate_out, 2, "s16", devices=devices)
     h.set_tracks(RAMPS64)
     assert bits_equal(h.process(x), want)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_effects_chain(xm, gpu, devices):
+    """xm_effects_create_multi: a batch of clips cut into contiguous blocks over
+    the device list, bit-identical to one device and to the oracle; host and
+    device memory, streaming, and effects added after creation."""
+    import torch
+    z = golden("effects.npz")
+    B, N = 7, 4410 + 13
+    x = np.stack([O.gen_f32(SEED, 1300 + b, 2, N) for b in range(B)])
+    h = np.linspace(-0.25, 0.5, 31).astype(np.float32)
+    one = xm.Effects(44100, 2)
+    multi = xm.Effects(44100, 2, devices=devices)
+    assert multi.n_devices() == len(devices)
+    for e in (one, multi):
+        for s in z["sos"]:
+            e.add_biquad(s)
+        e.add_fir(h)
+    want = one.process(x)
+    assert bits_equal(multi.process(x), want)
+    ref = np.stack([CO.fir_f32(CO.biquad_f32(x[b], z["sos"]), h) for b in range(B)])
+    assert bits_equal(want, ref)
+    md = xm.Effects(44100, 2, mem="device", devices=devices)
+    for s in z["sos"]:
+        md.add_biquad(s)
+    md.add_fir(h)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.zeros_like(xd)
+    md.process_ptrs([xd[b].data_ptr() for b in range(B)], [yd[b].data_ptr() for b in range(B)], N)
+    assert bits_equal(yd.cpu().numpy(), want)
+    multi.stream_reset(B)
+    parts = [multi.process_stream(x[:, a:b]) for a, b in ((0, 1), (1, 1), (1, 2000), (2000, N))]
+    assert bits_equal(np.concatenate(parts, axis=1), want)
+    with pytest.raises(xm.XmError) as e:
+        multi.set_stream(torch.cuda.current_stream().cuda_stream)
+    assert e.value.code == xm.XM_ENOSYS

@@ -11,7 +11,6 @@
 // FIR: upfirdn order (_upfirdn.py:107), taps staged in LDS, input tile in LDS.
 #include <stdlib.h>
 #include <algorithm>
-#include <atomic>
 #include "xm_device.h"
 
 // The LDS-DMA asm blocks set M0 themselves and list it as clobbered; clang
@@ -731,14 +730,7 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
                                        : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>));
     const int kpw = mf ? std::min(16 / j->n_sos * (4 / j->channels), BQ_KPW) : std::min(64 / j->n_sos, BQ_KPW);
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    static std::atomic<int> lds_set[8];            // per (kernel, C, ST) instantiation, set once per process
-    const int ki = mf * 4 + (j->channels == 2) * 2 + (j->state != nullptr);
-    if (!lds_set[ki].load(std::memory_order_acquire)) {
-        if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BQ_LDS) !=
-            hipSuccess)
-            return -1001;
-        lds_set[ki].store(1, std::memory_order_release);
-    }
+    if (xmh_func_lds((const void *)kern, (int)BQ_LDS)) return -1001;   // once per (kernel, device)
     XmhFxJob jj = *j;
     hipLaunchKernelGGL(kern, grid, dim3(128), BQ_LDS, (hipStream_t)stream, jj);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
@@ -766,9 +758,7 @@ extern "C" int xmh_launch_fx_fir(const XmhFxJob *j, void *stream)
         if (hipGetLastError() != hipSuccess) return -1001;
     }
     auto kern = j->channels == 1 ? k_fir<1> : k_fir<2>;
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return -1001;
+    if (lds > 64 * 1024 && xmh_func_lds((const void *)kern, (int)lds)) return -1001;
     hipLaunchKernelGGL(kern, grid, FIR_THREADS, lds, (hipStream_t)stream, *j);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }

@@ -436,9 +436,7 @@ template <typename K>
 int launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const XmhMixJob &j)
 {
     if (grid.x == 0 || grid.y == 0) return 0;
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return -1001;
+    if (lds > 64 * 1024 && xmh_func_lds((const void *)kern, (int)lds)) return -1001;   // once per (kernel, device)
     hipLaunchKernelGGL(kern, grid, block, lds, s, j);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess && getenv("XM_DEBUG")) fprintf(stderr, "generic launch: %s\n", hipGetErrorString(e));

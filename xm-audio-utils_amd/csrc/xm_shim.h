@@ -151,6 +151,11 @@ int  xmh_group_end(void);
 int  xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s);
 int  xmh_comm_check(void *comm);               /* XM_ECOMM on an asynchronous error */
 const char *xmh_arch_name(void);
+/* CUs of the current device (cached per device) */
+int  xmh_cu_count(void);
+/* hipFuncAttributeMaxDynamicSharedMemorySize >= bytes for kern on the current
+ * device, set once per (kernel, device) */
+int  xmh_func_lds(const void *kern, int bytes);
 
 /* ---------- kernels ----------------------------------------------------------- */
 /* resample (if rs.L != rs.M) + gain + ordered track sum; adds the launches

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
+#include <mutex>
 #include "xm_shim.h"
 
 #define XM_EDEVICE_ (-1001)
@@ -277,6 +278,51 @@ int xmh_comm_check(void *comm)
     ncclResult_t a = ncclSuccess;
     int rc = cmap(rccl().async_error((ncclComm_t)comm, &a), __LINE__);
     return rc ? rc : cmap(a, __LINE__);
+}
+
+// Per-device launch facts, cached (worker threads of a multi-device handle
+// reach these concurrently, each on its own device).
+namespace {
+constexpr int XMH_MAXDEV = 64;
+std::mutex g_attr_mu;
+struct LdsAttr {
+    const void *kern;
+    int dev, bytes;
+};
+LdsAttr g_lds[256];
+int g_n_lds = 0;
+int g_cus[XMH_MAXDEV];   // 0: not read yet
+}  // namespace
+
+int xmh_cu_count(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= XMH_MAXDEV) return 256;
+    std::lock_guard<std::mutex> g(g_attr_mu);
+    if (!g_cus[dev]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        g_cus[dev] = c;
+    }
+    return g_cus[dev];
+}
+
+int xmh_func_lds(const void *kern, int bytes)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return XM_EDEVICE_;
+    std::lock_guard<std::mutex> g(g_attr_mu);
+    for (int i = 0; i < g_n_lds; ++i)
+        if (g_lds[i].kern == kern && g_lds[i].dev == dev && g_lds[i].bytes >= bytes) return 0;
+    const int rc = map(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    if (rc) return rc;
+    for (int i = 0; i < g_n_lds; ++i)
+        if (g_lds[i].kern == kern && g_lds[i].dev == dev) {
+            g_lds[i].bytes = bytes;
+            return 0;
+        }
+    if (g_n_lds < (int)(sizeof g_lds / sizeof g_lds[0])) g_lds[g_n_lds++] = LdsAttr{kern, dev, bytes};
+    return 0;
 }
 
 const char *xmh_arch_name(void)

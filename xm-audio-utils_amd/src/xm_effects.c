@@ -36,6 +36,17 @@ struct XmEffects {
     int st_cur[XM_MAX_EFFECTS];
     size_t st_clips;
     int st_ready;
+    /* multi-device chain (xm_effects_create_multi / n_devices > 1): one
+     * single-device chain per entry of devs, a worker thread per device
+     * (src/xm_pool.c); a batch's clips are cut into contiguous blocks, block
+     * d on devs[d].  Clips are independent, so the result is the one-device
+     * result bit for bit.  The parent keeps the effect list (fx[]) and no
+     * device resources of its own. */
+    int n_sub;
+    int devs[XM_MAX_DEVICES];
+    XmEffects *sub[XM_MAX_DEVICES];
+    XmPool *pool;
+    size_t st_first[XM_MAX_DEVICES], st_cnt[XM_MAX_DEVICES];
 };
 
 XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status)
@@ -66,12 +77,57 @@ out:
     return e;
 }
 
+XmEffects *xm_effects_create_multi(const XmEffectsConfig *cfg, const int *devices, int n_devices, int *status)
+{
+    int rc = XM_OK;
+    XmEffects *e = NULL;
+    if (!cfg || !devices || n_devices < 1 || n_devices > XM_MAX_DEVICES || cfg->rate <= 0 ||
+        (cfg->channels != 1 && cfg->channels != 2) || (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE)) {
+        rc = XM_EINVAL;
+        goto out;
+    }
+    for (int d = 0; d < n_devices; ++d)
+        if (devices[d] < 0 || devices[d] >= xmh_device_count()) {
+            rc = XM_EDEVICE;
+            goto out;
+        }
+    e = calloc(1, sizeof *e);
+    if (!e) {
+        rc = XM_ENOMEM;
+        goto out;
+    }
+    e->cfg = *cfg;
+    e->cfg.device = devices[0];
+    e->n_sub = n_devices;
+    for (int d = 0; d < n_devices && !rc; ++d) {
+        XmEffectsConfig c = *cfg;
+        c.device = e->devs[d] = devices[d];
+        e->sub[d] = xm_effects_create_ex(&c, &rc);
+    }
+    if (!rc) e->pool = xm_pool_create(n_devices, e, &rc);
+out:
+    if (rc) xm_effects_freep(&e);
+    if (status) *status = rc;
+    return e;
+}
+
 XmEffects *xm_effects_create(int rate, int channels, int n_devices)
 {
-    if (n_devices != 1) return NULL;
     XmEffectsConfig c = {rate, channels, XM_MEM_HOST, 0};
-    return xm_effects_create_ex(&c, NULL);
+    if (n_devices == 1) return xm_effects_create_ex(&c, NULL);
+    if (n_devices < 1 || n_devices > XM_MAX_DEVICES) return NULL;
+    int devs[XM_MAX_DEVICES];
+    for (int d = 0; d < n_devices; ++d) devs[d] = d;
+    return xm_effects_create_multi(&c, devs, n_devices, NULL);
 }
+
+int xm_effects_n_devices(const XmEffects *e)
+{
+    if (!e) return XM_EINVAL;
+    return e->n_sub ? e->n_sub : 1;
+}
+
+int xm_effects_is_multi(const XmEffects *e) { return e && e->n_sub > 0; }
 
 static void free_stream_state(XmEffects *e)
 {
@@ -95,6 +151,14 @@ void xm_effects_freep(XmEffects **pe)
 {
     if (!pe || !*pe) return;
     XmEffects *e = *pe;
+    if (e->n_sub) {
+        xm_pool_free(&e->pool);
+        for (int d = 0; d < e->n_sub; ++d) xm_effects_freep(&e->sub[d]);
+        for (int i = 0; i < e->n_effects; ++i) free(e->fx[i].fir);
+        free(e);
+        *pe = NULL;
+        return;
+    }
     xmh_set_device(e->cfg.device);
     if (e->own_stream) xmh_stream_sync(e->own_stream);
     free_stages(e);
@@ -117,6 +181,10 @@ int xm_effects_add_biquad(XmEffects *e, const float sos[6])
         if (!isfinite(sos[i])) return XM_EINVAL;
     if (e->n_effects >= XM_MAX_EFFECTS) return XM_ENOMEM;
     /* a cascade longer than XM_MAX_SOS sections is split by the stager */
+    for (int d = 0; d < e->n_sub; ++d) {   /* multi-device: every device's chain */
+        const int rc = xm_effects_add_biquad(e->sub[d], sos);
+        if (rc) return rc;
+    }
     e->fx[e->n_effects].kind = 1;
     memcpy(e->fx[e->n_effects].sos, sos, sizeof(float) * 6);
     e->n_effects++;
@@ -178,6 +246,10 @@ int xm_effects_add_fir(XmEffects *e, const float *h, int K)
 {
     if (!e || !h || K < 1 || K > XM_MAX_FIR) return XM_EINVAL;
     if (e->n_effects >= XM_MAX_EFFECTS) return XM_ENOMEM;
+    for (int d = 0; d < e->n_sub; ++d) {   /* multi-device: every device's chain */
+        const int rc = xm_effects_add_fir(e->sub[d], h, K);
+        if (rc) return rc;
+    }
     float *c = malloc(sizeof(float) * (size_t)K);
     if (!c) return XM_ENOMEM;
     memcpy(c, h, sizeof(float) * (size_t)K);
@@ -201,12 +273,13 @@ int xm_effects_get_biquad(const XmEffects *e, int i, float sos[6])
 int xm_effects_set_stream(XmEffects *e, void *s)
 {
     if (!e) return XM_EINVAL;
+    if (e->n_sub) return XM_ENOSYS;   /* one stream per device, owned by the sub-chains */
     e->stream = s ? s : e->own_stream;
     e->user_stream = s != NULL;
     return XM_OK;
 }
 
-int xm_effects_device(const XmEffects *e) { return e ? e->cfg.device : -1; }
+int xm_effects_device(const XmEffects *e) { return e && !e->n_sub ? e->cfg.device : -1; }
 
 XmEffects *xm_effects_clone_on(const XmEffects *src, int device, int *status)
 {
@@ -261,6 +334,7 @@ static int build_stages(XmEffects *e)
 int xm_effects_stages(const XmEffects *ce, const XmFxStage **stages, int *n)
 {
     XmEffects *e = (XmEffects *)ce;   /* lazily built cache */
+    if (e->n_sub) return XM_EINVAL;   /* a multi-device chain has no stages of its own */
     int rc = build_stages(e);
     if (rc) return rc;
     *stages = e->stages;
@@ -409,11 +483,39 @@ static int process(XmEffects *e, const float *const *in, float *const *out, size
     return rc;
 }
 
+/* ---- multi-device dispatch: block d of the clips on sub-chain d ---------- */
+typedef struct {
+    const float *const *in;
+    float *const *out;
+    size_t batch, frames;
+    int stream;   /* 0 process_batch, 1 process_stream (blocks of stream_reset) */
+} XmFxArg;
+
+static int t_fx(void *ctx, int d, void *p)
+{
+    XmEffects *e = ctx;
+    const XmFxArg *a = p;
+    size_t f, c;
+    if (a->stream) {
+        f = e->st_first[d];
+        c = e->st_cnt[d];
+    } else {
+        xm_block(a->batch, e->n_sub, d, &f, &c);
+    }
+    if (!c) return XM_OK;
+    return a->stream ? xm_effects_process_stream(e->sub[d], a->in + f, a->out + f, c, a->frames)
+                     : xm_effects_process_batch(e->sub[d], a->in + f, a->out + f, c, a->frames);
+}
+
 int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const *out, size_t batch, size_t frames)
 {
     if (!e || (batch && (!in || !out))) return XM_EINVAL;
     if (batch == 0 || frames == 0) return XM_OK;
     if (batch > (size_t)INT32_MAX / 2) return XM_EINVAL;
+    if (e->n_sub) {
+        XmFxArg a = {in, out, batch, frames, 0};
+        return xm_pool_run(e->pool, t_fx, &a);
+    }
     int rc = xmh_set_device(e->cfg.device);
     if (!rc) rc = build_stages(e);
     if (rc) return rc;
@@ -424,6 +526,19 @@ int xm_effects_process_batch(XmEffects *e, const float *const *in, float *const 
 int xm_effects_stream_reset(XmEffects *e, size_t n_clips)
 {
     if (!e || n_clips == 0 || n_clips > (size_t)INT32_MAX / 2) return XM_EINVAL;
+    if (e->n_sub) {   /* device d streams block d of the clips */
+        int rc = XM_OK;
+        e->st_ready = 0;
+        for (int d = 0; d < e->n_sub && !rc; ++d) {
+            xm_block(n_clips, e->n_sub, d, &e->st_first[d], &e->st_cnt[d]);
+            if (e->st_cnt[d]) rc = xm_effects_stream_reset(e->sub[d], e->st_cnt[d]);
+        }
+        if (rc) return rc;
+        e->st_clips = n_clips;
+        e->st_ready = 1;
+        e->dirty = 0;
+        return XM_OK;
+    }
     int rc = xmh_set_device(e->cfg.device);
     if (!rc) rc = build_stages(e);
     if (rc) return rc;
@@ -458,6 +573,10 @@ int xm_effects_process_stream(XmEffects *e, const float *const *in, float *const
     if (!e || (n_clips && (!in || !out))) return XM_EINVAL;
     if (e->dirty || !e->st_ready || n_clips != e->st_clips) return XM_EINVAL;   /* reset first */
     if (frames == 0) return XM_OK;
+    if (e->n_sub) {
+        XmFxArg a = {in, out, n_clips, frames, 1};
+        return xm_pool_run(e->pool, t_fx, &a);
+    }
     int rc = xmh_set_device(e->cfg.device);
     if (rc) return rc;
     rc = process(e, in, out, n_clips, frames, 1);

@@ -39,8 +39,22 @@ int xm_effects_device(const XmEffects *e);
 /* the same chain (host coefficient copies replayed) on another device */
 XmEffects *xm_effects_clone_on(const XmEffects *src, int device, int *status);
 
-/* ---- multi-device mixer handles (src/xm_mixer_multi.c) ----------------- */
+/* ---- host worker pool of the multi-device handles (src/xm_pool.c) ------- */
 #define XM_MAX_DEVICES 16
+typedef struct XmPool XmPool;
+/* worker d runs task(ctx, d, arg); status of the first failing worker (in d order) */
+typedef int (*XmPoolTask)(void *ctx, int d, void *arg);
+XmPool *xm_pool_create(int n, void *ctx, int *status);   /* n == 1: runs on the caller's thread */
+void xm_pool_free(XmPool **p);
+int  xm_pool_run(XmPool *p, XmPoolTask t, void *arg);
+/* contiguous block d of n over `batch` items (the first batch % n blocks one longer) */
+void xm_block(size_t batch, int n, int d, size_t *first, size_t *cnt);
+
+/* ---- multi-device effects chains (src/xm_effects.c) ---------------------- */
+/* 1 if e is a multi-device chain (sub-chains per device) */
+int xm_effects_is_multi(const XmEffects *e);
+
+/* ---- multi-device mixer handles (src/xm_mixer_multi.c) ----------------- */
 typedef struct XmMulti XmMulti;
 /* one single-device sub-handle per entry of devs (duplicates allowed) */
 XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *status);

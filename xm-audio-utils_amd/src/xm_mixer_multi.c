@@ -15,18 +15,12 @@
  * of <= 64 Q15 terms are exact in any order, so the
  * collective's schedule cannot change a bit.
  */
-#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "xm_internal.h"
 
 typedef int (*XmTask)(XmMulti *mu, int d, void *arg);
-
-typedef struct XmWorker {
-    XmMulti *mu;
-    int d;
-} XmWorker;
 
 struct XmMulti {
     int n;
@@ -36,18 +30,10 @@ struct XmMulti {
     XmMixerConfig cfg;
     int n_tracks;
     XmTrackDesc tracks[XM_MAX_TRACKS]; /* the handle's full track list */
-    int span_mode;                     /* subs hold their config-5 track subsets */
-    /* worker pool (n > 1): worker d runs task(mu, d, arg) once per dispatch */
-    pthread_t th[XM_MAX_DEVICES];
-    XmWorker wk[XM_MAX_DEVICES];
-    int n_threads;
-    pthread_mutex_t lock;
-    pthread_cond_t go, done;
-    unsigned long gen;
-    int pending, quit;
-    XmTask task;
-    void *arg;
-    int rc[XM_MAX_DEVICES];
+    int span_mode;                     /* 0: every sub holds the full list; 1: sub d holds its
+                                          config-5 subset; 2: unknown (a failed update) */
+    XmPool *pool;                      /* worker d drives device d (src/xm_pool.c) */
+    int ran[XM_MAX_DEVICES];           /* sub d ran a call in the last dispatch (its timing counts) */
     /* streaming: the block of mixes each device streams */
     size_t st_first[XM_MAX_DEVICES], st_cnt[XM_MAX_DEVICES];
     int st_on;
@@ -59,58 +45,27 @@ struct XmMulti {
     size_t part_cap[XM_MAX_DEVICES], recv_cap[XM_MAX_DEVICES];
 };
 
-/* ---- worker pool -------------------------------------------------------- */
-static void *worker_main(void *p)
-{
-    XmWorker *w = p;
-    XmMulti *mu = w->mu;
-    unsigned long seen = 0;
-    pthread_mutex_lock(&mu->lock);
-    for (;;) {
-        while (!mu->quit && mu->gen == seen) pthread_cond_wait(&mu->go, &mu->lock);
-        if (mu->quit) break;
-        seen = mu->gen;
-        XmTask t = mu->task;
-        void *a = mu->arg;
-        pthread_mutex_unlock(&mu->lock);
-        int rc = t(mu, w->d, a);
-        pthread_mutex_lock(&mu->lock);
-        mu->rc[w->d] = rc;
-        if (--mu->pending == 0) pthread_cond_signal(&mu->done);
-    }
-    pthread_mutex_unlock(&mu->lock);
-    return NULL;
-}
-
 /* run task on every device (device d on worker d) and join; the first failing
  * device's status (in device order) is returned */
-static int run_all(XmMulti *mu, XmTask t, void *arg)
+typedef struct {
+    XmTask t;
+    void *arg;
+} XmTramp;
+
+static int tramp(void *ctx, int d, void *a)
 {
-    if (mu->n_threads == 0) {
-        for (int d = 0; d < mu->n; ++d) mu->rc[d] = t(mu, d, arg);
-    } else {
-        pthread_mutex_lock(&mu->lock);
-        mu->task = t;
-        mu->arg = arg;
-        mu->pending = mu->n;
-        mu->gen++;
-        pthread_cond_broadcast(&mu->go);
-        while (mu->pending) pthread_cond_wait(&mu->done, &mu->lock);
-        pthread_mutex_unlock(&mu->lock);
-    }
-    for (int d = 0; d < mu->n; ++d)
-        if (mu->rc[d]) return mu->rc[d];
-    return XM_OK;
+    const XmTramp *tr = a;
+    return tr->t((XmMulti *)ctx, d, tr->arg);
 }
 
-/* contiguous block of `batch` mixes for device d: the first batch % n blocks
- * hold one mix more */
-static void block(size_t batch, int n, int d, size_t *first, size_t *cnt)
+static int run_all(XmMulti *mu, XmTask t, void *arg)
 {
-    const size_t q = batch / (size_t)n, r = batch % (size_t)n;
-    *first = (size_t)d * q + ((size_t)d < r ? (size_t)d : r);
-    *cnt = q + ((size_t)d < r ? 1 : 0);
+    for (int d = 0; d < mu->n; ++d) mu->ran[d] = 0;   /* each task marks the subs it calls */
+    XmTramp tr = {t, arg};
+    return xm_pool_run(mu->pool, tramp, &tr);
 }
+
+static void block(size_t batch, int n, int d, size_t *first, size_t *cnt) { xm_block(batch, n, d, first, cnt); }
 
 static int fmt_bytes(int fmt) { return fmt == XM_FMT_S16 ? 2 : 4; }
 
@@ -138,9 +93,6 @@ XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *
     mu->n = n;
     mu->cfg = *cfg;
     mu->cfg.n_devices = 0;
-    pthread_mutex_init(&mu->lock, NULL);
-    pthread_cond_init(&mu->go, NULL);
-    pthread_cond_init(&mu->done, NULL);
     mu->distinct = 1;
     for (int d = 0; d < n; ++d) {
         mu->devs[d] = devs[d];
@@ -157,12 +109,7 @@ XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *
         mu->tracks[0].gain.gain0_q15 = mu->tracks[0].gain.gain1_q15 = 32768;
         mu->n_tracks = 1;
     }
-    for (int d = 0; d < n && !rc && n > 1; ++d) {
-        mu->wk[d].mu = mu;
-        mu->wk[d].d = d;
-        if (pthread_create(&mu->th[d], NULL, worker_main, &mu->wk[d])) rc = XM_ENOMEM;
-        else mu->n_threads++;
-    }
+    if (!rc) mu->pool = xm_pool_create(n, mu, &rc);
     if (rc) {
         xm_multi_free(mu);
         mu = NULL;
@@ -174,11 +121,7 @@ XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *
 void xm_multi_free(XmMulti *mu)
 {
     if (!mu) return;
-    pthread_mutex_lock(&mu->lock);
-    mu->quit = 1;
-    pthread_cond_broadcast(&mu->go);
-    pthread_mutex_unlock(&mu->lock);
-    for (int d = 0; d < mu->n_threads; ++d) pthread_join(mu->th[d], NULL);
+    xm_pool_free(&mu->pool);
     for (int d = 0; d < mu->n; ++d) {
         if (mu->comm[d]) xmh_comm_destroy(mu->comm[d]);
         xmh_set_device(mu->devs[d]);
@@ -187,9 +130,6 @@ void xm_multi_free(XmMulti *mu)
         xm_audio_mixer_freep(&mu->sub[d]);
         xm_effects_freep(&mu->fx[d]);
     }
-    pthread_cond_destroy(&mu->go);
-    pthread_cond_destroy(&mu->done);
-    pthread_mutex_destroy(&mu->lock);
     free(mu);
 }
 
@@ -202,22 +142,38 @@ int xm_multi_n_devices(const XmMulti *mu) { return mu->n; }
 static int set_full(XmMulti *mu)
 {
     int rc = XM_OK;
+    mu->span_mode = 2;
     for (int d = 0; d < mu->n && !rc; ++d) rc = xm_audio_mixer_set_tracks(mu->sub[d], mu->tracks, mu->n_tracks);
     if (!rc) mu->span_mode = 0;
     return rc;
 }
 
-static int ensure_full(XmMulti *mu) { return mu->span_mode ? set_full(mu) : XM_OK; }
+static int ensure_full(XmMulti *mu) { return mu->span_mode != 0 ? set_full(mu) : XM_OK; }
+
+/* install a new full list on every sub; on failure the handle keeps its
+ * previous list (re-applied to the subs), as a single-device handle does */
+static int replace_full(XmMulti *mu, const XmTrackDesc *tracks, int n_tracks)
+{
+    XmTrackDesc old[XM_MAX_TRACKS];
+    const int old_n = mu->n_tracks;
+    memcpy(old, mu->tracks, sizeof(XmTrackDesc) * (size_t)old_n);
+    if (tracks != mu->tracks) memcpy(mu->tracks, tracks, sizeof(XmTrackDesc) * (size_t)n_tracks);
+    mu->n_tracks = n_tracks;
+    int rc = set_full(mu);
+    if (rc) {
+        memcpy(mu->tracks, old, sizeof(XmTrackDesc) * (size_t)old_n);
+        mu->n_tracks = old_n;
+        set_full(mu);    /* best effort; on failure span_mode stays 2 and the next call retries */
+    }
+    return rc;
+}
 
 int xm_multi_set_tracks(XmMulti *mu, const XmTrackDesc *tracks, int n_tracks)
 {
     /* validate on the first sub-handle; the others see the same list */
     int rc = xm_audio_mixer_set_tracks(mu->sub[0], tracks, n_tracks);
-    if (rc) return rc;
-    memcpy(mu->tracks, tracks, sizeof(XmTrackDesc) * (size_t)n_tracks);
-    mu->n_tracks = n_tracks;
-    mu->span_mode = 1;   /* forces set_full over every sub */
-    return set_full(mu);
+    if (rc) return rc;   /* sub 0 kept its list (single-device rule) */
+    return replace_full(mu, tracks, n_tracks);
 }
 
 int xm_multi_set_crossfade(XmMulti *mu, int from, int to, int64_t start, int64_t len)
@@ -227,11 +183,10 @@ int xm_multi_set_crossfade(XmMulti *mu, int from, int to, int64_t start, int64_t
     if ((rc = xm_audio_mixer_set_crossfade(mu->sub[0], from, to, start, len))) return rc;
     /* sub 0 now holds the new list: give it to the others */
     int n = 0;
-    const XmTrackDesc *t = xm_mixer_tracks(mu->sub[0], &n);
-    memcpy(mu->tracks, t, sizeof(XmTrackDesc) * (size_t)n);
-    mu->n_tracks = n;
-    mu->span_mode = 1;
-    return set_full(mu);
+    XmTrackDesc t[XM_MAX_TRACKS];
+    const XmTrackDesc *t0 = xm_mixer_tracks(mu->sub[0], &n);
+    memcpy(t, t0, sizeof(XmTrackDesc) * (size_t)n);
+    return replace_full(mu, t, n);
 }
 
 int xm_multi_set_track_effects(XmMulti *mu, const XmEffects *fx)
@@ -257,6 +212,7 @@ int xm_multi_get_timing(const XmMulti *mu, XmMixerTiming *t)
 {
     memset(t, 0, sizeof *t);
     for (int d = 0; d < mu->n; ++d) {   /* devices run concurrently: the slowest one's times */
+        if (!mu->ran[d]) continue;      /* idle in the last call: its timing is an older call's */
         XmMixerTiming s;
         xm_audio_mixer_get_timing(mu->sub[d], &s);
         if (s.h2d_ms > t->h2d_ms) t->h2d_ms = s.h2d_ms;
@@ -285,6 +241,7 @@ static int t_batch(XmMulti *mu, int d, void *p)
     size_t f, c;
     block(a->batch, mu->n, d, &f, &c);
     if (!c) return XM_OK;
+    mu->ran[d] = 1;
     return xm_audio_mixer_process_batch(mu->sub[d], a->in + f * (size_t)mu->n_tracks, a->out + f, c, a->frames);
 }
 
@@ -302,6 +259,7 @@ static int t_strided(XmMulti *mu, int d, void *p)
     size_t f, c;
     block(a->batch, mu->n, d, &f, &c);
     if (!c) return XM_OK;
+    mu->ran[d] = 1;
     const char *in = (const char *)a->in1 + (ptrdiff_t)f * a->ms * in_elem(&mu->cfg);
     char *out = (char *)a->out1 + (ptrdiff_t)f * a->os * out_elem(&mu->cfg);
     return xm_audio_mixer_process_strided(mu->sub[d], in, a->ts, a->ms, out, a->os, c, a->frames);
@@ -330,6 +288,7 @@ static int t_sharded(XmMulti *mu, int d, void *p)
 {
     const XmShardArg *a = p;
     if (!a->batch[d]) return XM_OK;
+    mu->ran[d] = 1;
     return xm_audio_mixer_process_strided(mu->sub[d], a->in[d], a->ts, a->ms, a->out[d], a->os, a->batch[d],
                                           a->frames);
 }
@@ -349,6 +308,7 @@ static int t_timeline(XmMulti *mu, int d, void *p)
     size_t f, c;
     block(a->batch, mu->n, d, &f, &c);
     if (!c) return XM_OK;
+    mu->ran[d] = 1;
     return xm_audio_mixer_process_timeline(mu->sub[d], a->in + f * (size_t)mu->n_tracks, a->place, a->out + f, c,
                                            a->frames);
 }
@@ -397,6 +357,7 @@ static int t_stream(XmMulti *mu, int d, void *p)
     XmStreamArg *a = p;
     a->got[d] = 0;
     if (!mu->st_cnt[d]) return XM_OK;
+    mu->ran[d] = 1;
     const char *in = a->in ? (const char *)a->in + (ptrdiff_t)mu->st_first[d] * a->ms * in_elem(&mu->cfg)
                            : NULL;
     char *out = a->out ? (char *)a->out + (ptrdiff_t)mu->st_first[d] * a->os * out_elem(&mu->cfg) : NULL;
@@ -448,6 +409,7 @@ static int t_span(XmMulti *mu, int d, void *p)
     const XmSpanArg *a = p;
     XmAudioMixer *s = mu->sub[d];
     const size_t blk = a->nb * a->S;   /* int32 per owned block */
+    mu->ran[d] = 1;
     int rc = xmh_set_device(mu->devs[d]);
     if (rc) return rc;
     if (a->phase == 0) {
@@ -487,8 +449,9 @@ int xm_multi_mix_spanning_s16(XmMulti *mu, const void *const *in, ptrdiff_t ts, 
         if (!in[d] || !out[d]) return XM_EINVAL;
     if (batch == 0) return XM_OK;
     const int per = mu->n_tracks / n;
-    if (!mu->span_mode) {   /* sub d holds its own tracks */
+    if (mu->span_mode != 1) {   /* sub d holds its own tracks */
         int rc = XM_OK;
+        mu->span_mode = 2;
         for (int d = 0; d < n && !rc; ++d) rc = xm_audio_mixer_set_tracks(mu->sub[d], mu->tracks + d * per, per);
         if (rc) {
             set_full(mu);

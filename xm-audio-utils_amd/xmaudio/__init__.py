@@ -64,7 +64,7 @@ EXPORTED = [
     "xm_audio_mixer_stream_flush", "xm_effects_stream_reset", "xm_effects_process_stream",
     "xm_audio_mixer_process_timeline",
     "xm_audio_mixer_create_multi", "xm_audio_mixer_n_devices", "xm_audio_mixer_process_sharded",
-    "xm_audio_mixer_mix_spanning_s16",
+    "xm_audio_mixer_mix_spanning_s16", "xm_effects_create_multi", "xm_effects_n_devices",
 ]
 
 
@@ -144,6 +144,9 @@ _sigs = {
                                             C.c_ssize_t, C.POINTER(_sz), _sz]),
     "xm_audio_mixer_mix_spanning_s16": (_i, [_vp, C.POINTER(_vp), C.c_ssize_t, C.c_ssize_t, C.POINTER(_vp),
                                              C.c_ssize_t, _sz, _sz]),
+    "xm_effects_create": (_vp, [_i, _i, _i]),
+    "xm_effects_create_multi": (_vp, [C.POINTER(XmEffectsConfig), C.POINTER(_i), _i, C.POINTER(_i)]),
+    "xm_effects_n_devices": (_i, [_vp]),
 }
 for _n, (_r, _a) in _sigs.items():
     if os.environ.get("XM_AUDIO_LIB") and not hasattr(_lib, _n):
@@ -405,13 +408,21 @@ class Mixer:
 class Effects:
     """xm_effects_* handle."""
 
-    def __init__(self, rate: int, channels: int = 2, mem: str = "host", device: int = 0):
+    def __init__(self, rate: int, channels: int = 2, mem: str = "host", device: int = 0, devices=None):
+        """devices: a device list -> multi-device chain (xm_effects_create_multi)."""
         cfg = XmEffectsConfig(rate, channels, MEM[mem], device)
         st = C.c_int(0)
-        self._h = _lib.xm_effects_create_ex(C.byref(cfg), C.byref(st))
+        if devices is not None:
+            dl = (C.c_int * len(devices))(*devices)
+            self._h = _lib.xm_effects_create_multi(C.byref(cfg), dl, len(devices), C.byref(st))
+        else:
+            self._h = _lib.xm_effects_create_ex(C.byref(cfg), C.byref(st))
         if not self._h:
             raise XmError(st.value, "xm_effects_create")
         self.channels = channels
+
+    def n_devices(self) -> int:
+        return _lib.xm_effects_n_devices(self._h)
 
     # module globals may already be gone at interpreter exit: bind what close needs
     def close(self, _vp=C.c_void_p, _byref=C.byref, _free=_lib.xm_effects_freep):
