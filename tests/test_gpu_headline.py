@@ -135,3 +135,26 @@ def test_fast_split_pointer_table(xm, gpu):
     xs, got = x.cpu().numpy(), y.cpu().numpy()
     for b in (0, 5, 15):
         assert bits_equal(got[b], CO.resample_f32(xs[perm[b]], 147, 160)), b
+
+
+def test_split_production_grid_first_last_clip(xm, gpu):
+    """Config 2 at its production size (BASELINE.json:8): 4096 stereo 10 s
+    fp32 clips resampled 48k -> 44.1k in split mode (8 clips per pseudo-mix
+    on the fused kernel, 512 pseudo-mixes); the first and last clip of each
+    end of the grid bit-compared with the oracle, nothing left unwritten."""
+    import torch
+    from bench import SEED
+    B, N = 4096, 480000
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks([dict(gain0=1.0)])
+    F = m.out_frames(N)
+    x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B, 2, N)
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N)
+    torch.cuda.synchronize()
+    t = m.timing()
+    assert t.n_launches == 1 and t.fast_launches == 1, (t.n_launches, t.fast_launches)
+    for b in (0, 7, 8, B - 8, B - 1):
+        assert bits_equal(y[b].cpu().numpy(), CO.resample_f32(x[b].cpu().numpy(), 147, 160)), b
+    assert not bool(y.isnan().any())

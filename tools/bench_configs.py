@@ -23,6 +23,9 @@ oconv   the headline with XM_MIXER_OUT_CONVERT: s16 output (fused kernel epilogu
 Unit: input samples (frames x channels x tracks) per second; roofline
 fraction = algorithmic bytes (inputs once + output once) / kernel time / 8 TB/s.
 Inputs are synthetic PCM generated in HBM (xm_synth_pcm), outside the timing.
+After timing, every line bit-checks the first and the last mix (or clip) of
+its batch against the C oracle (oracle/xm_oracle.c) and reports
+parity_check (--no-check skips it).
 """
 import argparse
 import json
@@ -33,9 +36,12 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "xm-audio-utils_amd"))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import xmaudio as xm  # noqa: E402
 from bench import RAMPS, SEED, HBM_PEAK_GBS  # noqa: E402
+import c_oracle as CO  # noqa: E402
 
 Q15_RAMPS = [dict(gain0_q15=29491), dict(gain0_q15=0, gain1_q15=26214, ramp_start=0, ramp_len=48000),
              dict(gain0_q15=22938, gain1_q15=6554, ramp_start=240000, ramp_len=96000), dict(gain0_q15=16384),
@@ -63,6 +69,24 @@ def timed(step, steps, warmup, stream):
     return wall * 1e3, e0.elapsed_time(e1) / steps
 
 
+def beq(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def to_s16(y):
+    return np.clip(np.rint(y.astype(np.float32) * np.float32(32768.0)), -32768, 32767).astype(np.int16)
+
+
+def ends(n):
+    return sorted({0, n - 1})
+
+
+def parity(args, fn):
+    """fn() -> bool, run after timing unless --no-check (None then)."""
+    return None if args.no_check else bool(fn())
+
+
 def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, **extra):
     line = {"config": name, "workload": workload, "value": round(samples / (wall_ms * 1e-3) / 1e6, 1),
             "unit": "Msamples/s", "ms_per_step": round(wall_ms, 4), "kernel_ms": round(ker_ms, 4),
@@ -84,7 +108,10 @@ def c2(a):
     xm.synth(x.data_ptr(), "f32", SEED, 0, B, 2, N, 0, s.cuda_stream)
     m.set_stream(s.cuda_stream)
     w, k = timed(lambda: m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N), a.steps, a.warmup, s)
-    report("c2", f"48k->44.1k resample, {B} stereo 10 s fp32 clips", B * N * 2, B * N * 8 + B * F * 8, w, k, m)
+    ok = parity(a, lambda: all(beq(y[b].cpu().numpy(), CO.resample_f32(x[b].cpu().numpy(), 147, 160))
+                               for b in ends(B)))
+    report("c2", f"48k->44.1k resample, {B} stereo 10 s fp32 clips", B * N * 2, B * N * 8 + B * F * 8, w, k, m,
+           parity_check=ok, fast_launches=m.timing().fast_launches)
 
 
 def c3(a):
@@ -98,8 +125,10 @@ def c3(a):
     m.set_stream(s.cuda_stream)
     w, k = timed(lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), N * 2, B, N),
                  a.steps, a.warmup, s)
+    ok = parity(a, lambda: beq(y[ends(B)].cpu().numpy(), CO.batch_mix_s16(x[ends(B)].cpu().numpy(), Q15_RAMPS,
+                                                                               threads=8)[0]))
     report("c3", f"8-track s16 Q15 ramp/crossfade mix, {B} mixes x 10 s stereo 48 kHz", B * ntr * N * 2,
-           B * ntr * N * 4 + B * N * 4, w, k, m)
+           B * ntr * N * 4 + B * N * 4, w, k, m, parity_check=ok)
 
 
 def c4(a):
@@ -118,8 +147,17 @@ def c4(a):
     m.set_stream(s.cuda_stream)
     w, k = timed(lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N),
                  a.steps, a.warmup, s)
+    sos = np.stack([fx.biquad(i) for i in range(len(EQ5))])
+
+    def chk():
+        for b in ends(B):
+            xb = x[b].cpu().numpy()
+            r = [CO.biquad_f32(CO.resample_f32(xb[t], 147, 160), sos) for t in range(ntr)]
+            if not beq(y[b].cpu().numpy(), CO.mix_f32(r, RAMPS)):
+                return False
+        return True
     report("c4", f"resample + 5-band EQ + 8-track mix, {B * ntr} clips per GPU (config 4 shard of 8192/8)",
-           B * ntr * N * 2, B * ntr * N * 8 + B * F * 8, w, k, m)
+           B * ntr * N * 2, B * ntr * N * 8 + B * F * 8, w, k, m, parity_check=parity(a, chk))
 
 
 def c5(a):
@@ -140,11 +178,16 @@ def c5(a):
     y = torch.empty((B // rk.world, N, 2), dtype=torch.int16, device="cuda")
     w, k = timed(lambda: xd.mix_spanning_s16(rk, m, x, out=y), a.steps, a.warmup, s)
     w = xd.max_over_ranks(rk, w, device="cuda")
+    ok = None
+    if rk.world == 1:   # one rank: the partial over its 8 tracks is the whole mix
+        ok = parity(a, lambda: beq(y[ends(B)].cpu().numpy(),
+                                   CO.batch_mix_s16(x[ends(B)].cpu().numpy(), Q15_RAMPS, threads=8)[0]))
     if rk.rank == 0:
         report("c5", f"64-track s16 mixdown, {B} mixes x 10 s stereo 48 kHz, 8 tracks per GPU, "
                      f"{rk.world} GPU(s) (partial + reduce-scatter + saturate)",
                rk.world * B * ntr * N * 2, B * ntr * N * 4 + (B // rk.world) * N * 4, w, k, m,
-               note="per-GPU HBM bytes: this GPU's tracks once + its finished mixes once")
+               note="per-GPU HBM bytes: this GPU's tracks once + its finished mixes once; bench.py --config c5 "
+                    "is the full 64-track line", parity_check=ok)
     xd.finish(rk)
 
 
@@ -186,10 +229,34 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
         step = lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)  # noqa: E731
     w, k = timed(step, a.steps, a.warmup, s)
     fast = m.timing().fast_launches
+    launches = m.timing().n_launches
+
+    def chk():
+        from math import gcd
+        g = gcd(fi, fo)
+        L, M = fo // g, fi // g
+        for b in ends(B):
+            xb = x[b].cpu().numpy()                     # [ntr][N][2] (planar: [ntr][2][N] in memory order)
+            if planar:
+                xb = np.ascontiguousarray(xb.reshape(ntr, 2, N).swapaxes(1, 2))
+            if fmt == "s16":
+                want = CO.resample_mix_s16(list(xb), Q15_RAMPS, L, M)
+            else:
+                xf = xb.astype(np.float32) * np.float32(2.0 ** -15) if conv else xb
+                want = CO.resample_mix_f32(list(xf), RAMPS, L, M)
+                if oconv:
+                    want = to_s16(want)
+            got = (ys[b, :F] if stream else y[b]).cpu().numpy()
+            if planar:
+                got = np.ascontiguousarray(got.reshape(2, F).T)
+            if not beq(got, want):
+                return False
+        return True
     report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix"
            + (f", {ofmt} out" if oconv else ""),
            B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m,
-           kernel="k_rs147_mix" if fast else "generic")
+           kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
+           parity_check=parity(a, chk))
 
 
 def odd(a): _shape(a, "odd", N=480001)
@@ -212,6 +279,7 @@ def main():
     ap.add_argument("--mixes4", type=int, default=128)
     ap.add_argument("--mixes5", type=int, default=512)
     ap.add_argument("--mixes", type=int, default=512, help="headline-shaped variants")
+    ap.add_argument("--no-check", action="store_true", help="skip the post-timing oracle checks")
     a = ap.parse_args()
     for w in a.which:
         globals()[w](a)
