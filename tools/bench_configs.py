@@ -160,6 +160,63 @@ def c4(a):
            B * ntr * N * 2, B * ntr * N * 8 + B * F * 8, w, k, m, parity_check=parity(a, chk))
 
 
+def fir(a):
+    """FIR effect alone: K-tap filter over 1024 stereo 10 s clips @ 44.1 kHz,
+    device memory, out of place (k_fir_rb)."""
+    B, N, K = a.clips_fx, 441000, a.fir_k
+    h = (np.sin(np.arange(K, dtype=np.float64) * 0.37) / (1 + np.arange(K))).astype(np.float32)
+    e = xm.Effects(44100, 2, mem="device")
+    e.add_fir(h)
+    x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+    y = torch.empty_like(x)
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B, 2, N, 0, s.cuda_stream)
+    e.set_stream(s.cuda_stream)
+    ins, outs = [x[b].data_ptr() for b in range(B)], [y[b].data_ptr() for b in range(B)]
+    w, k = timed(lambda: e.process_ptrs(ins, outs, N), a.steps, a.warmup, s)
+    ok = parity(a, lambda: all(beq(y[b].cpu().numpy(), CO.fir_f32(x[b].cpu().numpy(), h)) for b in ends(B)))
+    alg = 2 * B * N * 2 * 4
+    line = {"config": "fir", "workload": f"{K}-tap FIR (upfirdn order), {B} stereo 10 s fp32 clips @ 44.1 kHz",
+            "value": round(B * N * 2 / (w * 1e-3) / 1e6, 1), "unit": "Msamples/s", "ms_per_step": round(w, 4),
+            "kernel_ms": round(k, 4),
+            "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved_GBps": round(alg / (k * 1e-3) / 1e9, 1),
+                         "frac": round(alg / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "valu_floor_note": "2K separately rounded fp32 ops per output sample"},
+            "parity_check": ok}
+    print(json.dumps(line), flush=True)
+
+
+def bq(a):
+    """Config 4's biquad stage alone: the 5-band EQ cascade over 1024 stereo
+    10 s clips @ 44.1 kHz, device memory, in place (k_biquad_pc)."""
+    B, N = a.clips_fx, 441000
+    e = xm.Effects(44100, 2, mem="device")
+    for band in EQ5:
+        e.add_eq_band(*band)
+    sos = np.stack([e.biquad(i) for i in range(len(EQ5))])
+    x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B, 2, N, 0, s.cuda_stream)
+    x0 = x[ends(B)].clone()
+    e.set_stream(s.cuda_stream)
+    ptrs = [x[b].data_ptr() for b in range(B)]
+    # one checked pass, then timed passes (in place: each pass filters the previous output)
+    e.process_ptrs(ptrs, ptrs, N)
+    torch.cuda.synchronize()
+    ok = parity(a, lambda: all(beq(x[b].cpu().numpy(), CO.biquad_f32(x0[i].cpu().numpy(), sos))
+                               for i, b in enumerate(ends(B))))
+    w, k = timed(lambda: e.process_ptrs(ptrs, ptrs, N), a.steps, a.warmup, s)
+    alg = 2 * B * N * 2 * 4
+    line = {"config": "bq", "workload": f"5-section biquad cascade (sosfilt order), {B} stereo 10 s fp32 clips",
+            "value": round(B * N * 2 / (w * 1e-3) / 1e6, 1), "unit": "Msamples/s", "ms_per_step": round(w, 4),
+            "kernel_ms": round(k, 4),
+            "roofline": {"bound": "serial recurrence (latency per wave), HBM roofline quoted", "alg_bytes": alg,
+                         "achieved_GBps": round(alg / (k * 1e-3) / 1e9, 1),
+                         "frac": round(alg / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "parity_check": ok}
+    print(json.dumps(line), flush=True)
+
+
 def c5(a):
     """Config 5 per GPU: 8 of the 64 s16 tracks of every mix live here; int32
     partial -> RCCL reduce-scatter (torchrun, N > 1) -> saturate."""
@@ -280,6 +337,8 @@ def main():
     ap.add_argument("--mixes5", type=int, default=512)
     ap.add_argument("--mixes", type=int, default=512, help="headline-shaped variants")
     ap.add_argument("--no-check", action="store_true", help="skip the post-timing oracle checks")
+    ap.add_argument("--clips-fx", type=int, default=1024, help="fir / bq: clips")
+    ap.add_argument("--fir-k", type=int, default=63, help="fir: taps")
     a = ap.parse_args()
     for w in a.which:
         globals()[w](a)

@@ -28,6 +28,6 @@ if fn is not None:
     fn(buf.ctypes.data_as(ctypes.c_void_p))
     w = buf.reshape(2048, 2).astype(np.float64)
     w = w[w[:, 0] > 0]                         # the launch's workgroups
-    steps = (N + 127) // 128 + 4
+    steps = (N + 127) // 128 + 4   # k_biquad_lane geometry
     print("compute wave, cycles per 128-frame step: chunk %.0f  barrier/wait %.0f" % tuple(w.mean(0) / steps),
           flush=True)

@@ -615,6 +615,262 @@ __global__ __launch_bounds__(128) void k_biquad_lane(XmhFxJob j)
     }
 }
 
+// ---- producer / chain split: k_biquad_pc ------------------------------------
+// The recurrence of one (clip, section, channel) needs 4 dependent ops per
+// frame, but sosfilt's 9 include 3 feed-forward products b_r * x that do not
+// depend on the state.  k_biquad_lane issues all 9 on the one wave whose
+// serial speed is the whole kernel's time (5/6 of the SIMDs are idle: 1024
+// clips x 5 sections x 2 channels is 171 waves).  Here a producer wave forms
+// the products one step ahead with plain v_mul_f32 (IEEE-exact, the very
+// products sosfilt takes) and hands them to the chain wave through LDS, so
+// the chain wave issues 6 VALU per frame (o = p0 + z0; t = (-a1)*o;
+// t = p1 + t; z0 = z1 + t; u = (-a2)*o; z1 = p2 + u -- bq_mf_pair's order,
+// the same ops as bq_lane_pair bit for bit).  Three waves per workgroup:
+//   chain (wave 0): lane = (clip, section, channel) as k_biquad_lane; section
+//     s filters chunk c = i - 2s - 1 at step i from its product row
+//     P[lane][(i-1) & 1] ([frame][p0 p1 p2], read by ds_read_b128) into its own
+//     planar output row O[lane][i & 1] (ds_write_b128);
+//   producer (wave 1): lane (clip, s, ch) forms the products of chunk i - 2s
+//     into P[lane][i & 1] from section s-1's output row O[lane-4][(i-1) & 1]
+//     (section 0: the interleaved input chunk inb[i & 1]), and the last
+//     section's lanes interleave their chain's previous output row into
+//     outb[i & 1];
+//   copy (wave 2): every HBM access, by per-lane 64-bit addresses: the DMA of
+//     chunk i + 1 (global_load_lds_dwordx4, 4 / C clips per instruction) and
+//     the stores of outb[(i - 1) & 1] (chunk i - 1 - 2 ns).
+// One barrier per step; chunks are 64 frames.  Rows are skewed by 4 floats
+// per lane so the 16-B row accesses of a wave are bank-conflict free.
+constexpr int PC_CH = 64;                          // frames per chunk (per channel)
+constexpr int PC_KPW = 12;                         // clips per workgroup at most
+constexpr int PC_PS = 2 * PC_CH * 3 + 4;           // floats per lane: P[parity][frame][3] + skew
+constexpr int PC_OS = 2 * PC_CH + 4;               // floats per lane: O[parity][frame] + skew
+constexpr int PC_O0 = 64 * PC_PS;                  // O rows (floats); P rows start at 0
+constexpr int PC_IN0 = PC_O0 + 64 * PC_OS;         // inb[parity][clip]: chunks of PC_CH * C floats, contiguous
+constexpr int PC_OUT0 = PC_IN0 + 2 * PC_KPW * PC_CH * 2;   // outb, same layout
+constexpr size_t PC_LDS = (size_t)(PC_OUT0 + 2 * PC_KPW * PC_CH * 2) * 4;   // 157,696 B
+static_assert(PC_LDS <= 160 * 1024, "one workgroup per CU");
+static_assert(PC_PS % 64 == 4 && PC_OS % 64 == 4 && PC_IN0 % 4 == 0, "16-B rows, 4-float skew per lane");
+
+template <int C>
+__device__ __forceinline__ void pc_copy_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, int ns,
+                                             float *lf)
+{
+    typedef const __attribute__((address_space(1))) float gcf;
+    typedef __attribute__((address_space(1))) float gf;
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int CB = PC_CH * C * 4;              // chunk bytes per clip
+    constexpr int LPC = CB / 16;                   // lanes per clip chunk
+    constexpr int CPI = 64 / LPC;                  // clips per DMA instruction
+    constexpr int NG = PC_KPW / CPI;               // instruction groups at most
+    const int lane = threadIdx.x & 63;
+    const int64_t N = j.frames;
+    const int64_t nchunk = (N + PC_CH - 1) / PC_CH, nfull = N / PC_CH;
+    const int ng = (nclip + CPI - 1) / CPI;
+    const int kl = lane / LPC;                     // this lane's clip within a group
+    uint64_t xa[NG], ya[NG];
+    const float *xp[NG];
+    float *yp[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int k = min(g * CPI + kl, nclip - 1);   // loads of missing clips fill unused rows
+        xp[g] = j.in_ptrs[clip0 + k];
+        yp[g] = j.out_ptrs[clip0 + k];
+        xa[g] = (uint64_t)(uintptr_t)xp[g] + (uint64_t)(lane % LPC) * 16u;
+        ya[g] = (uint64_t)(uintptr_t)yp[g] + (uint64_t)(lane % LPC) * 16u;
+    }
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)lf);
+    auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
+        if (c >= nchunk) return;
+        const int p = (int)(c & 1);
+        if (c < nfull) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (g >= ng) break;                // wave-uniform
+                const uint32_t m0 = lds0 + (uint32_t)(PC_IN0 + (p * PC_KPW + g * CPI) * PC_CH * C) * 4u;
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                             :
+                             : "s"(m0), "v"(xa[g] + (uint64_t)c * CB)
+                             : "memory", "m0");
+            }
+            return;
+        }
+        // partial last chunk: element loads with bounds, zero past N
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            if (g >= ng) break;
+            const int64_t s0 = c * PC_CH * C + (int64_t)(lane % LPC) * 4;
+            f4 v = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (s0 + e < N * C) v[e] = ((gcf *)xp[g])[s0 + e];
+            *(f4 *)(lf + PC_IN0 + (p * PC_KPW + g * CPI) * PC_CH * C + lane * 4) = v;
+        }
+    };
+    auto store_chunk = [&](int64_t c, int p) __attribute__((always_inline)) {
+        if (c < 0 || c >= nchunk) return;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            if (g >= ng) break;
+            const f4 v = *(const f4 *)(lf + PC_OUT0 + (p * PC_KPW + g * CPI) * PC_CH * C + lane * 4);
+            if (g * CPI + kl >= nclip) continue;   // a clamped lane: not its clip
+            if (c < nfull) {
+                asm volatile("global_store_dwordx4 %0, %1, off" : : "v"(ya[g] + (uint64_t)c * CB), "v"(v) : "memory");
+            } else {
+                const int64_t s0 = c * PC_CH * C + (int64_t)(lane % LPC) * 4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (s0 + e < N * C) ((gf *)yp[g])[s0 + e] = v[e];
+            }
+        }
+    };
+    load_chunk(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int64_t i = 0; i < steps; ++i) {
+        load_chunk(i + 1);
+        store_chunk(i - 1 - 2 * ns, (int)((i - 1) & 1));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk i + 1 landed (and the stores left)
+        __syncthreads();
+    }
+}
+
+template <int C, bool ST>
+__global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
+{
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int CPG = 4 / C;                     // clips per group (a block of 4 lanes)
+    extern __shared__ bq_f4 bq_lds[];
+    float *lf = (float *)bq_lds;
+    const int ns = j.n_sos;
+    const int gpw = 16 / ns;                       // groups per wave
+    const int kpw = min(gpw * CPG, PC_KPW);        // clips per workgroup
+    const int clip0 = blockIdx.x * kpw;
+    const int nclip = min(kpw, j.n_clips - clip0);
+    const int64_t N = j.frames;
+    const int64_t nchunk = (N + PC_CH - 1) / PC_CH;
+    const int64_t steps = nchunk + 2 * ns + 1;
+    const int wave = threadIdx.x >> 6;
+    if (wave == 2) {
+        pc_copy_wave<C>(j, clip0, nclip, steps, ns, lf);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int blk = lane >> 2, r = lane & 3;
+    const int grp = blk / ns, s = blk % ns, ci = r / C, ch = r % C;
+    const int kk = grp * CPG + ci;
+    const bool valid = blk < gpw * ns && kk < nclip;
+    const float *q = j.sos + 6 * (valid ? s : 0);
+    const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
+    const int P_lane = lane * PC_PS, O_lane = PC_O0 + lane * PC_OS;
+
+    if (wave == 1) {
+        // ---------------- producer: products one step ahead ------------------
+        const bool last = valid && s == ns - 1;
+        const int kq = valid ? kk : 0;
+        __syncthreads();
+        for (int64_t i = 0; i < steps; ++i) {
+            const int par = (int)(i & 1);
+            // source of chunk i - 2s: section s - 1's output row, or the input
+            int src, stride;
+            if (valid && s == 0) {
+                src = PC_IN0 + (par * PC_KPW + kq) * PC_CH * C + ch;
+                stride = C;
+            } else {
+                src = (valid ? O_lane - 4 * PC_OS : O_lane) + (par ^ 1) * PC_CH;   // lane - 4 = section s - 1
+                stride = 1;
+            }
+            float *Pw = lf + P_lane + par * PC_CH * 3;
+#pragma unroll 4
+            for (int qd = 0; qd < PC_CH / 4; ++qd) {
+                float x[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[e] = lf[src + (4 * qd + e) * stride];
+                f4 w0, w1, w2;
+                w0 = f4{b0 * x[0], b1 * x[0], b2 * x[0], b0 * x[1]};
+                w1 = f4{b1 * x[1], b2 * x[1], b0 * x[2], b1 * x[2]};
+                w2 = f4{b2 * x[2], b0 * x[3], b1 * x[3], b2 * x[3]};
+                f4 *pw = (f4 *)(Pw + 12 * qd);
+                pw[0] = w0;
+                pw[1] = w1;
+                pw[2] = w2;
+            }
+            if (last) {   // the last section's previous output -> outb[i & 1], interleaved
+                const f4 *Or = (const f4 *)(lf + O_lane + (par ^ 1) * PC_CH);
+                float *ob = lf + PC_OUT0 + (par * PC_KPW + kq) * PC_CH * C + ch;
+#pragma unroll 4
+                for (int qd = 0; qd < PC_CH / 4; ++qd) {
+                    const f4 v = Or[qd];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ob[(4 * qd + e) * C] = v[e];
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+
+    // ---------------- chain: 6 VALU per frame ---------------------------------
+    const float na1 = -a1, na2 = -a2;              // (-a)*o == -(a*o): IEEE negation is exact
+    float z0 = 0.0f, z1 = 0.0f;
+    float *st = (ST && valid) ? j.state + ((size_t)(clip0 + kk) * ns + s) * 2 * C : nullptr;
+    if (ST && st) {
+        z0 = st[ch];
+        z1 = st[C + ch];
+    }
+    __syncthreads();
+    for (int64_t i = 0; i < steps; ++i) {
+        const int64_t c = i - 2 * s - 1;           // chunk this lane filters
+        const bool act = valid && c >= 0 && c < nchunk;
+        const float z0s = z0, z1s = z1;
+        const int par = (int)(i & 1);
+        const float *Pr = lf + P_lane + (par ^ 1) * PC_CH * 3;
+        float *Ow = lf + O_lane + par * PC_CH;
+        const bool tail = ST && st && act && (c + 1) * PC_CH > N;
+        if (__builtin_amdgcn_ballot_w64(tail) != 0) {
+            // a streamed block's last chunk: frames past N are padding and must
+            // not advance the state (wave-uniform branch)
+            for (int f = 0; f < PC_CH; ++f) {
+                const float p0 = Pr[3 * f], p1 = Pr[3 * f + 1], p2 = Pr[3 * f + 2];
+                const float o = p0 + z0;
+                if (!(tail && c * PC_CH + f >= N)) {
+                    z0 = z1 + (p1 + na1 * o);
+                    z1 = p2 + na2 * o;
+                }
+                Ow[f] = o;
+            }
+        } else {
+            // quads of 4 frames (12 products = 3 x 16 B), read two quads ahead
+            const f4 *P4 = (const f4 *)Pr;
+            f4 A0 = P4[0], A1 = P4[1], A2 = P4[2];
+            f4 B0 = P4[3], B1 = P4[4], B2 = P4[5];
+#pragma unroll
+            for (int qd = 0; qd < PC_CH / 4; ++qd) {
+                f4 N0, N1, N2;
+                if (qd + 2 < PC_CH / 4) {
+                    N0 = P4[3 * (qd + 2)];
+                    N1 = P4[3 * (qd + 2) + 1];
+                    N2 = P4[3 * (qd + 2) + 2];
+                }
+                const float pa[4] = {A0[0], A0[1], A0[2], 0.0f}, pb[4] = {A0[3], A1[0], A1[1], 0.0f};
+                const float pc[4] = {A1[2], A1[3], A2[0], 0.0f}, pd[4] = {A2[1], A2[2], A2[3], 0.0f};
+                float o[4];
+                bq_mf_pair(pa, pb, z0, z1, na1, na2, o[0], o[1]);
+                bq_mf_pair(pc, pd, z0, z1, na1, na2, o[2], o[3]);
+                ((f4 *)Ow)[qd] = f4{o[0], o[1], o[2], o[3]};
+                A0 = B0; A1 = B1; A2 = B2;
+                if (qd + 2 < PC_CH / 4) { B0 = N0; B1 = N1; B2 = N2; }
+            }
+        }
+        if (!act) { z0 = z0s; z1 = z1s; }
+        __syncthreads();                           // products of step i + 1 ready; outputs visible
+    }
+    if (ST && st) {
+        st[ch] = z0;
+        st[C + ch] = z1;
+    }
+}
+
 constexpr int FIR_THREADS = 256;
 constexpr int FIR_OPT = 4;
 constexpr int FIR_CHUNK = FIR_THREADS * FIR_OPT;
@@ -662,6 +918,162 @@ __global__ __launch_bounds__(FIR_THREADS) void k_fir(XmhFxJob j)
 #pragma unroll
         for (int c = 0; c < C; ++c) y[n * C + c] = acc[o][c];
     }
+}
+
+// ---- FIR, register-blocked: k_fir_rb ----------------------------------------
+// upfirdn order per output: acc = +0, then acc = acc + x[n-K+1+t] * h[K-1-t]
+// for t ascending.  A workgroup (4 waves) stages the input tile of its 1792
+// output frames plus the K-1 frames before them in LDS with 16-B loads (the
+// chunk grid of the absolute address: no per-element division), the left edge
+// zero (or the streamed history).  Lane l of wave w owns FU = 7 consecutive
+// outputs, so the 7 outputs of a tap share 6 of their 7 window frames: the
+// window lives in registers (two 7-frame halves A, B that swap roles every
+// 7-tap block, no moves), one LDS read per frame per 7 outputs x 7 taps, and
+// each tap's coefficient h[K-1-t] is wave-uniform (scalar loads, an SGPR
+// operand).  Stereo (L, R) ride in packed pairs: per output and tap one
+// v_pk_mul_f32 + one v_pk_add_f32.  A lane stride of 7 frames (an odd number
+// of 8-B frames) puts the 32 lanes of each ds_read_b64 half-wave on 32
+// distinct bank pairs.  Outputs go back through wave-private LDS so the
+// stores are whole 16-B chunks in frame order.
+constexpr int FR_U = 7;                            // outputs per lane (odd: conflict-free reads)
+constexpr int FR_WAVES = 4;
+constexpr int FR_TILE = 64 * FR_U * FR_WAVES;      // output frames per workgroup (1792)
+
+template <int C>
+struct FrV;
+template <>
+struct FrV<1> { typedef float T; };
+template <>
+struct FrV<2> { typedef float T __attribute__((ext_vector_type(2))); };
+
+template <int C>
+__global__ __launch_bounds__(64 * FR_WAVES) void k_fir_rb(XmhFxJob j)
+{
+    typedef typename FrV<C>::T V;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) f4 gcf4;
+    typedef __attribute__((address_space(1))) f4 gf4;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int K = j.fir_len;
+    const int clip = blockIdx.y;
+    const float *x = j.in_ptrs[clip];
+    float *y = j.out_ptrs[clip];
+    const int64_t N = j.frames;
+    const int64_t n0 = (int64_t)blockIdx.x * FR_TILE;
+    const int64_t f0 = n0 - K + 1;                 // first tile frame
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // the tile: floats [f0*C, (n0 + FR_TILE + 14)*C) of the clip (14 frames of
+    // slack for the window's read-ahead), on the 16-B grid of absolute addresses
+    const uint64_t xa = (uint64_t)(uintptr_t)x;
+    // tile float i <-> clip float g0 + i, at LDS float i + sh, where sh puts
+    // the LDS 16-B chunks on the 16-B grid of absolute addresses; a stereo
+    // clip that is not 8-B aligned (frames would straddle) loads float by float
+    const bool al = C == 1 || (xa & 7) == 0;
+    const int64_t g0 = f0 * C;                     // clip float of tile float 0
+    const int sh = al ? (int)((((int64_t)((xa >> 2) & 3) + g0) % 4 + 4) % 4) : 0;
+    const int tile_f = (FR_TILE + K - 1 + 14) * C;
+    float *tile = lds;                             // LDS floats [0, sh + tile_f) (rounded to 16 B)
+    const int nchunk = (sh + tile_f + 3) / 4;
+    const int64_t clip_hi = N * C;                 // clip floats
+    for (int q = tid; q < nchunk; q += 64 * FR_WAVES) {
+        const int64_t gi = g0 - sh + 4 * (int64_t)q;   // clip float of the chunk's first float
+        f4 v;
+        if (al && gi >= 0 && gi + 4 <= clip_hi) {
+            v = *(gcf4 *)(x + gi);                 // a 16-B aligned chunk of the clip
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t g = gi + e;
+                float u = 0.0f;
+                if (g >= 0 && g < clip_hi) u = x[g];
+                else if (g < 0 && g >= g0 && j.hist_in)   // streaming: the K-1 frames before this block
+                    u = j.hist_in[(int64_t)clip * (K - 1) * C + (K - 1) * C + g];
+                v[e] = u;
+            }
+        }
+        *(f4 *)(tile + 4 * q) = v;
+    }
+    __syncthreads();
+
+    const V *tv = (const V *)(tile + sh);          // tile frames (V = one frame)
+    const int base = w * 64 * FR_U + lane * FR_U;  // tile frame of tap 0 of this lane's first output
+    const float *h = j.fir;
+    V acc[FR_U], A[FR_U], B[FR_U];
+#pragma unroll
+    for (int u = 0; u < FR_U; ++u) {
+        acc[u] = V(0.0f);
+        A[u] = tv[base + u];
+        B[u] = tv[base + FR_U + u];
+    }
+    // one 7-tap block: acc[u] += W[u + t] * h[K-1-(tb+t)], W = P ++ Q (frames tb .. tb+13)
+    auto block = [&](const V (&P)[FR_U], const V (&Q)[FR_U], int tb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < FR_U; ++t) {
+            const float hv = h[K - 1 - (tb + t)];  // wave-uniform
+#pragma unroll
+            for (int u = 0; u < FR_U; ++u) {
+                const V xv = u + t < FR_U ? P[u + t] : Q[u + t - FR_U];
+                acc[u] = acc[u] + xv * hv;
+            }
+        }
+    };
+    int tb = 0;
+    for (; tb + 2 * FR_U <= K; tb += 2 * FR_U) {
+        block(A, B, tb);
+#pragma unroll
+        for (int u = 0; u < FR_U; ++u) A[u] = tv[base + tb + 2 * FR_U + u];
+        block(B, A, tb + FR_U);
+#pragma unroll
+        for (int u = 0; u < FR_U; ++u) B[u] = tv[base + tb + 3 * FR_U + u];
+    }
+    if (tb + FR_U <= K) {                          // one more whole block: then the window is B ++ next
+        block(A, B, tb);
+#pragma unroll
+        for (int u = 0; u < FR_U; ++u) {
+            A[u] = B[u];
+            B[u] = tv[base + tb + 2 * FR_U + u];
+        }
+        tb += FR_U;
+    }
+    // the last K - tb (< 7) taps, window A ++ B
+    const int rem = K - tb;
+#pragma unroll
+    for (int t = 0; t < FR_U - 1; ++t) {
+        if (t >= rem) break;                       // wave-uniform
+        const float hv = h[K - 1 - (tb + t)];
+#pragma unroll
+        for (int u = 0; u < FR_U; ++u) {
+            const V xv = u + t < FR_U ? A[u + t] : B[u + t - FR_U];
+            acc[u] = acc[u] + xv * hv;
+        }
+    }
+    // outputs -> wave-private LDS (after the whole workgroup is done with the
+    // tile) -> whole 16-B chunks in frame order
+    __syncthreads();
+    V *ov = (V *)lds + w * 64 * FR_U;
+#pragma unroll
+    for (int u = 0; u < FR_U; ++u) ov[lane * FR_U + u] = acc[u];
+    const int64_t wn0 = n0 + w * 64 * FR_U;        // this wave's first output frame
+    const float *of = (const float *)ov;
+    const int64_t og0 = wn0 * C;                   // clip float of the wave's first output float
+    constexpr int OWF = 64 * FR_U * C;             // floats per wave
+    const int osh = (int)(((uint64_t)(uintptr_t)(y + og0) >> 2) & 3);   // floats before a 16-B boundary
+    const int lead = osh ? 4 - osh : 0;
+    for (int i = lane; i < lead; i += 64)          // unaligned head, element by element
+        if (og0 + i < N * C) y[og0 + i] = of[i];
+    for (int q = lane; 4 * q + lead + 4 <= OWF; q += 64) {
+        const int i = lead + 4 * q;
+        if (og0 + i + 4 <= N * C) {
+            *(gf4 *)(y + og0 + i) = f4{of[i], of[i + 1], of[i + 2], of[i + 3]};
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (og0 + i + e < N * C) y[og0 + i + e] = of[i + e];
+        }
+    }
+    const int body = lead + ((OWF - lead) / 4) * 4;
+    for (int i = body + lane; i < OWF; i += 64)    // tail
+        if (og0 + i < N * C) y[og0 + i] = of[i];
 }
 
 // Streaming FIR: the K-1 frames that precede the next block, from the old
@@ -724,6 +1136,18 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
 #else
     constexpr bool MFP = false;
 #endif
+#ifndef XM_BQ_LANE
+    if (mf && !MFP) {   // the product path: producer / chain split (k_biquad_pc)
+        auto pk = j->channels == 2 ? (j->state ? k_biquad_pc<2, true> : k_biquad_pc<2, false>)
+                                   : (j->state ? k_biquad_pc<1, true> : k_biquad_pc<1, false>);
+        const int kpw = std::min(16 / j->n_sos * (4 / j->channels), PC_KPW);
+        if (xmh_func_lds((const void *)pk, (int)PC_LDS)) return -1001;   // once per (kernel, device)
+        XmhFxJob jj = *j;
+        hipLaunchKernelGGL(pk, dim3((unsigned)((j->n_clips + kpw - 1) / kpw)), dim3(192), PC_LDS,
+                           (hipStream_t)stream, jj);
+        return hipGetLastError() == hipSuccess ? 0 : -1001;
+    }
+#endif
     auto kern = mf ? (j->channels == 2 ? (j->state ? k_biquad_lane<2, true, MFP> : k_biquad_lane<2, false, MFP>)
                                        : (j->state ? k_biquad_lane<1, true, MFP> : k_biquad_lane<1, false, MFP>))
                    : (j->channels == 2 ? (j->state ? k_biquad_pipe<2, true> : k_biquad_pipe<2, false>)
@@ -757,6 +1181,18 @@ extern "C" int xmh_launch_fx_fir(const XmhFxJob *j, void *stream)
                            (hipStream_t)stream, *j);
         if (hipGetLastError() != hipSuccess) return -1001;
     }
+#ifndef XM_FIR_OLD
+    {   // the register-blocked kernel (k_fir_rb)
+        const size_t rl = ((size_t)(FR_TILE + K - 1 + 14) * j->channels + 8) * sizeof(float);
+        const size_t lds_rb = std::max(rl, (size_t)FR_TILE * j->channels * sizeof(float));
+        if (lds_rb > 160 * 1024) return -1003;
+        auto kr = j->channels == 1 ? k_fir_rb<1> : k_fir_rb<2>;
+        if (lds_rb > 64 * 1024 && xmh_func_lds((const void *)kr, (int)lds_rb)) return -1001;
+        hipLaunchKernelGGL(kr, dim3((unsigned)((j->frames + FR_TILE - 1) / FR_TILE), (unsigned)j->n_clips),
+                           64 * FR_WAVES, lds_rb, (hipStream_t)stream, *j);
+        return hipGetLastError() == hipSuccess ? 0 : -1001;
+    }
+#endif
     auto kern = j->channels == 1 ? k_fir<1> : k_fir<2>;
     if (lds > 64 * 1024 && xmh_func_lds((const void *)kern, (int)lds)) return -1001;
     hipLaunchKernelGGL(kern, grid, FIR_THREADS, lds, (hipStream_t)stream, *j);

@@ -398,9 +398,12 @@ static int run_chain(XmEffects *e, size_t batch, size_t frames, float **src, flo
         return rc;
     }
     /* FIR reads neighbours of the samples it writes: never run it in place.
-     * If any clip is processed in place, first copy the inputs to buf0. */
-    int inplace = 0, off = 0;
-    for (size_t i = 0; i < batch; ++i) inplace |= src[i] == dst[i];
+     * If any clip is processed in place and the chain has a FIR stage, first
+     * copy the inputs to buf0.  A biquad cascade runs in place (each chunk is
+     * read into LDS before its outputs are stored). */
+    int inplace = 0, off = 0, has_fir = 0;
+    for (int s = 0; s < e->n_stages; ++s) has_fir |= e->stages[s].kind == 2;
+    for (size_t i = 0; has_fir && i < batch; ++i) inplace |= src[i] == dst[i];
     void **cur = T_src;
     if (inplace) {
         for (size_t i = 0; !rc && i < batch; ++i)
