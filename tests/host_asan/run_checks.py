@@ -111,6 +111,25 @@ def main():
     outs.append(m.stream_flush())
     check("streaming resample+mix == whole signal", beq(np.concatenate(outs, axis=1), ref))
 
+    # device-memory streaming with blocks large enough for the direct bulk
+    # (the fused bulk reads the caller's block; the window keeps only the head
+    # and the tail): ragged blocks, whole-signal bits
+    xs3 = f32_tracks(2, 8, 4001, base=150)
+    dm = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    dm.set_tracks(RAMPS)
+    Fs = dm.out_frames(4001)
+    ys3 = np.zeros((2, Fs + 8, 2), np.float32)
+    dm.stream_begin(2)
+    got, pos = 0, 0
+    for nb in (1500, 3, 1200, 1298):
+        blk = np.ascontiguousarray(xs3[:, :, pos:pos + nb])
+        got += dm.stream_push_strided(blk.ctypes.data, nb * 2, 8 * nb * 2, nb, ys3[:, got:].ctypes.data,
+                                      (Fs + 8) * 2, Fs + 8 - got)
+        pos += nb
+    got += dm.stream_flush_strided(ys3[:, got:].ctypes.data, (Fs + 8) * 2, Fs + 8 - got)
+    check("device-memory streaming, direct bulk == whole signal",
+          got == Fs and beq(ys3[:, :Fs], CO.batch_resample_mix_f32(xs3, RAMPS, 147, 160)[0]))
+
     # timeline: per-track rates and placement
     tl = xm.Mixer(44100, 48000, 1, "f32")
     tl.set_tracks([dict(in_rate=22050, gain0=0.7), dict(in_rate=16000, gain0=0.4), dict(gain0=0.5)])

@@ -853,6 +853,25 @@ static int st_fast_part(XmAudioMixer *m, XmhMixJob *j, int64_t R, const char *wi
     return XM_OK;
 }
 
+/* Device-memory pushes of the 147/160 stream: the super-period-aligned bulk
+ * of the release reads the caller's block itself (no copy into the window).
+ * The bulk starts at the first super-period boundary ob_al >= st_out whose
+ * input frame a0 = 160*ob_al/147 has its 32-frame lead-in inside the block
+ * (a0 - 32 >= B0, the block's first absolute frame); the outputs before ob_al
+ * (the head) and everything of small blocks still run from the window.
+ * Returns ob_al, or -1 when the bulk is too small to pay (the window path). */
+static int64_t st_direct_cut(const XmAudioMixer *m, int64_t B0, int64_t R, int64_t mend, int flush)
+{
+    const int64_t L = m->table.d.L, M = m->table.d.M;
+    if (flush || m->cfg.mem_kind != XM_MEM_DEVICE || L != 147 || M != 160 || !m->table.fast || io_flags(m))
+        return -1;
+    int64_t ob_al = (m->st_out + L - 1) / L * L;
+    const int64_t q = (B0 + 32 + M - 1) / M;   /* first SP whose input frame a0 = q*M has its lead-in in the block */
+    if (q * L > ob_al) ob_al = q * L;
+    if (mend - ob_al < 4 * L || ob_al / L * M >= R) return -1;
+    return ob_al;
+}
+
 static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, size_t n, void *out,
                    ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush)
 {
@@ -876,10 +895,15 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     if (rc) return rc;
     begin_call(m);
     if ((rc = upload_gains(m))) return rc;
-    /* 1) append the block to the window */
+    /* direct bulk (device memory): the window takes only the head's input,
+     * frames [B0, a0 + 16) (the last head output reads up to a0 + 10) */
+    const int64_t B0 = m->st_recv;
+    const int64_t ob_dir = nout ? st_direct_cut(m, B0, R, mend, flush) : -1;
+    const size_t n_app = ob_dir >= 0 ? (size_t)(ob_dir / 147 * 160 + 16 - B0) : n;
+    /* 1) append the block (or the head's part of it) to the window */
     const size_t keep = (size_t)(m->st_recv - m->st_w0);
-    if (keep + n > m->st_cap) {
-        size_t cap = keep + n + (keep + n) / 4 + 64;
+    if (keep + n_app > m->st_cap) {
+        size_t cap = keep + n_app + (keep + n_app) / 4 + 64;
         void *nw[2] = {NULL, NULL};
         rc = xmh_malloc(&nw[0], rows * cap * fb);
         if (!rc) rc = xmh_malloc(&nw[1], rows * cap * fb);
@@ -900,13 +924,13 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     }
     char *win = (char *)m->st_win[m->st_cur];
     const size_t pitch = m->st_cap * fb;
-    if (n) {
+    if (n_app) {
         if (ms == (ptrdiff_t)ntr * ts || batch == 1)
-            rc = xmh_memcpy2d(win + keep * fb, pitch, in, (size_t)ts * (size_t)elem, n * fb, rows, m->stream);
+            rc = xmh_memcpy2d(win + keep * fb, pitch, in, (size_t)ts * (size_t)elem, n_app * fb, rows, m->stream);
         else
             for (size_t b = 0; !rc && b < batch; ++b)
                 rc = xmh_memcpy2d(win + (b * (size_t)ntr * pitch) + keep * fb, pitch,
-                                  (const char *)in + (ptrdiff_t)b * ms * elem, (size_t)ts * (size_t)elem, n * fb,
+                                  (const char *)in + (ptrdiff_t)b * ms * elem, (size_t)ts * (size_t)elem, n_app * fb,
                                   (size_t)ntr, m->stream);
         if (rc) return rc;
     }
@@ -928,7 +952,44 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
         j.out_mix_stride = host ? (int64_t)(nout * (size_t)C) : (int64_t)os;
         int launches = 0;
         rc = xmh_event_record(m->ev[2], m->stream);
-        if (!rc) rc = st_fast_part(m, &j, R, win, fb, &launches);   /* the super-period-aligned bulk */
+        if (!rc && ob_dir >= 0) {
+            /* the bulk [ob_dir, mend) on the fused kernel, straight from the
+             * caller's block: window job at input frame a0, its 32 lead-in
+             * frames real samples, ramps shifted by ob_dir */
+            const int64_t a0 = ob_dir / 147 * 160;
+            XmhGain g[XM_MAX_TRACKS];
+            for (int t = 0; t < m->n_tracks; ++t) {
+                g[t] = m->gains[t];
+                g[t].start -= ob_dir;
+            }
+            XmhMixJob w = j;
+            w.in = (const char *)in + (size_t)(a0 - B0) * fb;
+            w.in_track_stride = ts;
+            w.in_mix_stride = ms;
+            w.frames_in = R - a0;
+            w.frames_out = mend - ob_dir;
+            w.in_base = w.out_base = 0;
+            w.out = (char *)j.out + (size_t)(ob_dir - m->st_out) * ofb;
+            w.gains_host = g;
+            w.rs.fast = m->table.fast;
+            w.window = 1;
+            w.unity = m->unity;
+            rc = xmh_launch_mix_window(&w, m->stream, &launches, &m->timing.fast_launches);
+            if (rc == XM_ENOSYS) {   /* not the fused kernel's shape: the bulk on the generic kernel, same block */
+                XmhMixJob gj = j;
+                gj.in = in;
+                gj.in_track_stride = ts;
+                gj.in_mix_stride = ms;
+                gj.in_base = B0;
+                gj.out_base = ob_dir;
+                gj.frames_out = mend - ob_dir;
+                gj.out = w.out;
+                rc = xmh_launch_mix(&gj, m->stream, &launches, &m->timing.fast_launches);
+            }
+            j.frames_out = ob_dir - m->st_out;                     /* the head: from the window */
+        } else if (!rc) {
+            rc = st_fast_part(m, &j, R, win, fb, &launches);       /* the super-period-aligned bulk */
+        }
         if (!rc && j.frames_out)                                   /* the rest: generic kernel */
             rc = xmh_launch_mix(&j, m->stream, &launches, &m->timing.fast_launches);
         m->timing.n_launches += launches;
@@ -949,7 +1010,24 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     int64_t w0 = st_first_needed(m, mend) - (m->table.d.L == 147 && m->table.d.M == 160 ? 32 : 0);
     if (w0 > R) w0 = R;
     if (w0 < m->st_w0) w0 = m->st_w0;
-    if (w0 > m->st_w0 && !flush) {
+    if (ob_dir >= 0 && w0 >= B0) {
+        /* the window kept only the head's input: the frames the next release
+         * needs, [w0, R), come from the caller's block */
+        const size_t left = (size_t)(R - w0);
+        char *nwin = (char *)m->st_win[m->st_cur ^ 1];
+        if (left > m->st_cap) return XM_EINVAL;   /* cannot happen: w0 >= R - 32 - T - M/L */
+        if (ms == (ptrdiff_t)ntr * ts || batch == 1)
+            rc = xmh_memcpy2d(nwin, pitch, (const char *)in + (size_t)(w0 - B0) * fb, (size_t)ts * (size_t)elem,
+                              left * fb, rows, m->stream);
+        else
+            for (size_t b = 0; !rc && b < batch; ++b)
+                rc = xmh_memcpy2d(nwin + b * (size_t)ntr * pitch, pitch,
+                                  (const char *)in + (ptrdiff_t)b * ms * elem + (size_t)(w0 - B0) * fb,
+                                  (size_t)ts * (size_t)elem, left * fb, (size_t)ntr, m->stream);
+        if (rc) return rc;
+        m->st_cur ^= 1;
+        m->st_w0 = w0;
+    } else if (w0 > m->st_w0 && !flush) {
         const size_t left = (size_t)(R - w0);
         if (left)
             rc = xmh_memcpy2d(m->st_win[m->st_cur ^ 1], pitch, win + (size_t)(w0 - m->st_w0) * fb, pitch,
