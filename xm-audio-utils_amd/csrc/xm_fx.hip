@@ -1005,11 +1005,11 @@ __global__ __launch_bounds__(64 * FR_WAVES) void k_fir_rb(XmhFxJob j)
         A[u] = tv[base + u];
         B[u] = tv[base + FR_U + u];
     }
-    // one 7-tap block: acc[u] += W[u + t] * h[K-1-(tb+t)], W = P ++ Q (frames tb .. tb+13)
-    auto block = [&](const V (&P)[FR_U], const V (&Q)[FR_U], int tb) __attribute__((always_inline)) {
+    // one 7-tap block: acc[u] += W[u + t] * hb[t], W = P ++ Q (frames tb .. tb+13)
+    auto block = [&](const V (&P)[FR_U], const V (&Q)[FR_U], const float *hb) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < FR_U; ++t) {
-            const float hv = h[K - 1 - (tb + t)];  // wave-uniform
+            const float hv = hb[t];                // wave-uniform (SGPR)
 #pragma unroll
             for (int u = 0; u < FR_U; ++u) {
                 const V xv = u + t < FR_U ? P[u + t] : Q[u + t - FR_U];
@@ -1017,17 +1017,35 @@ __global__ __launch_bounds__(64 * FR_WAVES) void k_fir_rb(XmhFxJob j)
             }
         }
     };
+    // the 14 coefficients of a loop iteration, h[K-1-t] for t = tb .. tb+13:
+    // the contiguous taps h[K-14-tb .. K-1-tb] by wide scalar loads, issued
+    // one iteration ahead of their use (past the last iteration the block
+    // start clamps to tap 0: loaded, never used)
+    auto coefs = [&](float (&hc)[2 * FR_U], int tb) __attribute__((always_inline)) {
+        const float *hb = h + max(K - 2 * FR_U - tb, 0);
+        float blk[2 * FR_U];
+#pragma unroll
+        for (int i = 0; i < 2 * FR_U; ++i) blk[i] = hb[i];
+#pragma unroll
+        for (int i = 0; i < 2 * FR_U; ++i) hc[i] = blk[2 * FR_U - 1 - i];
+    };
     int tb = 0;
+    float hc[2 * FR_U];
+    coefs(hc, 0);
     for (; tb + 2 * FR_U <= K; tb += 2 * FR_U) {
-        block(A, B, tb);
+        float hn[2 * FR_U];
+        coefs(hn, tb + 2 * FR_U);
+        block(A, B, hc);
 #pragma unroll
         for (int u = 0; u < FR_U; ++u) A[u] = tv[base + tb + 2 * FR_U + u];
-        block(B, A, tb + FR_U);
+        block(B, A, hc + FR_U);
 #pragma unroll
         for (int u = 0; u < FR_U; ++u) B[u] = tv[base + tb + 3 * FR_U + u];
+#pragma unroll
+        for (int i = 0; i < 2 * FR_U; ++i) hc[i] = hn[i];
     }
     if (tb + FR_U <= K) {                          // one more whole block: then the window is B ++ next
-        block(A, B, tb);
+        block(A, B, hc);
 #pragma unroll
         for (int u = 0; u < FR_U; ++u) {
             A[u] = B[u];
