@@ -101,7 +101,9 @@ def test_s16_tracks_into_f32_mix(xm, gpu, rates, planar, convert_out):
     m.set_tracks(RAMPS)
     y = m.process(_planar(x) if planar else x)
     assert y.dtype == (np.int16 if convert_out else np.float32)
-    assert m.timing().fast_launches == 0
+    # 4-track 48k->44.1k interleaved mixes run on the fused kernel's 8-row
+    # s16 layout (phantom rows); planar s16 tracks, and 48k->48k, do not
+    assert m.timing().fast_launches == (1 if fi != fo and not planar else 0)
     xf = x.astype(np.float32) * np.float32(2.0 ** -15)
     for b in range(B):
         ref = CO.resample_mix_f32(list(xf[b]), RAMPS, 147, 160) if fi != fo else CO.mix_f32(list(xf[b]), RAMPS)
