@@ -90,7 +90,7 @@ def test_fast_layouts_device_strides_tables_s16_out(xm, gpu, nt):
     m.process_ptrs(ins, outs, B, N)
     torch.cuda.synchronize()
     assert m.timing().fast_launches == 1
-    ref2, _ = CO.batch_resample_mix_f32(x[:, perm], [ramps[p] for p in perm], 147, 160, threads=4)
+    ref2, _ = CO.batch_resample_mix_f32(x[:, perm], ramps, 147, 160, threads=4)   # gains follow the slot
     got = y2.cpu().numpy()
     for b in range(B):
         o = b if outs[1] - outs[0] == F * 8 else (3 * b) % B
