@@ -86,14 +86,14 @@ def test_fast_layouts_device_strides_tables_s16_out(xm, gpu, nt):
     if nt <= 8 and 8 // max(1, 1 << (nt - 1).bit_length()) > 1:
         outs = [y2[b].data_ptr() for b in range(B)]   # several mixes per wave: a strided output table
     else:
-        outs = [y2[(3 * b) % B].data_ptr() for b in range(B)]
+        outs = [y2[(5 * b + 2) % B].data_ptr() for b in range(B)]   # a permutation of the rows
     m.process_ptrs(ins, outs, B, N)
     torch.cuda.synchronize()
     assert m.timing().fast_launches == 1
     ref2, _ = CO.batch_resample_mix_f32(x[:, perm], ramps, 147, 160, threads=4)   # gains follow the slot
     got = y2.cpu().numpy()
     for b in range(B):
-        o = b if outs[1] - outs[0] == F * 8 else (3 * b) % B
+        o = b if outs[1] - outs[0] == F * 8 else (5 * b + 2) % B
         assert bits_equal(got[o], ref2[b]), b
     # s16 output
     c = xm.Mixer(48000, 44100, 2, "f32", convert_out=True)
