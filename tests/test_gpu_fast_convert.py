@@ -51,6 +51,7 @@ def test_fast_split_convert_out(xm, gpu):
     xm.synth(x.data_ptr(), "f32", SEED, 91, B, 2, N)
     x[:, 500:700] *= 3.0               # saturating clips
     y = torch.full((B, F, 2), 0x5a5a, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
     m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N)
     t = m.timing()
     assert t.fast_launches == 1, (t.n_launches, t.fast_launches)

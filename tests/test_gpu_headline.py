@@ -24,6 +24,7 @@ def _run(xm, B, N, ramps):
     x = torch.empty((B, 8, N, 2), dtype=torch.float32, device="cuda")
     y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
     xm.synth(x.data_ptr(), "f32", SEED, 0, B * 8, 2, N)
+    torch.cuda.synchronize()
     m.process_strided(x.data_ptr(), N * 2, 8 * N * 2, y.data_ptr(), F * 2, B, N)
     t = m.timing()
     assert t.n_launches == 1 and t.fast_launches == 1, (t.n_launches, t.fast_launches)
@@ -69,6 +70,7 @@ def test_fast_split_odd_lengths(xm, gpu, N):
     x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
     xm.synth(x.data_ptr(), "f32", SEED, 77, B, 2, N)
     y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
     m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N)
     t = m.timing()
     assert t.fast_launches == 1, (t.n_launches, t.fast_launches)
@@ -151,6 +153,7 @@ def test_split_production_grid_first_last_clip(xm, gpu):
     x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
     xm.synth(x.data_ptr(), "f32", SEED, 0, B, 2, N)
     y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
     m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N)
     torch.cuda.synchronize()
     t = m.timing()

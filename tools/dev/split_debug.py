@@ -14,6 +14,7 @@ for B, N in ((4096, 480000), (512, 480000), (4096, 48000), (1024, 480000)):
     x = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
     xm.synth(x.data_ptr(), "f32", 0x584D4155, 0, B, 2, N)
     y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
     m.process_strided(x.data_ptr(), N * 2, N * 2, y.data_ptr(), F * 2, B, N)
     torch.cuda.synchronize()
     t = m.timing()

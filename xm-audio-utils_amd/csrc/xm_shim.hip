@@ -66,8 +66,11 @@ void xmh_host_free(void *p)
 
 int xmh_stream_create(void **s)
 {
+    // a blocking stream: a handle's own stream is ordered after work the
+    // caller queued on the legacy default stream (a memset or fill of the
+    // output, a generator), as the caller of a synchronous call expects
     hipStream_t h = nullptr;
-    int rc = map(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
+    int rc = map(hipStreamCreateWithFlags(&h, hipStreamDefault));
     *s = (void *)h;
     return rc;
 }
