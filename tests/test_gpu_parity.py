@@ -195,6 +195,23 @@ def test_effects_biquad_fir_golden(xm, gpu):
     assert bits_equal(g.process(z["x"][None, :1000, :1])[0, :, 0], z["y_fir7_mono"])
 
 
+@pytest.mark.parametrize("C", [1, 2])
+def test_fir_tap_counts_vs_c_oracle(xm, gpu, C):
+    """The register-blocked FIR over every shape of its tap loop: fewer taps
+    than one 7-tap block, whole 14-tap iterations, a trailing whole block and
+    a remainder, and more taps than one tile; clip lengths off the 1792-frame
+    tile and the 16-B grid."""
+    rng = np.random.default_rng(11)
+    for K in (1, 2, 6, 7, 8, 13, 14, 15, 20, 21, 27, 28, 35, 63, 64, 127, 255, 2000):
+        for N in (1, 5, 1791 + K, 4001):
+            x = O.gen_f32(SEED, 3000 + K, C, N)
+            h = rng.standard_normal(K).astype(np.float32) / K
+            e = xm.Effects(48000, C)
+            e.add_fir(h)
+            y = e.process(x[None])[0]
+            assert bits_equal(y, CO.fir_f32(x, h)), (K, N)
+
+
 def test_effects_chain_vs_c_oracle(xm, gpu):
     z = golden("effects.npz")
     x = np.stack([O.gen_f32(SEED, 900 + b, 2, 20000) for b in range(6)])

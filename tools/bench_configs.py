@@ -87,10 +87,10 @@ def parity(args, fn):
     return None if args.no_check else bool(fn())
 
 
-def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, **extra):
+def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, launches=None, **extra):
     line = {"config": name, "workload": workload, "value": round(samples / (wall_ms * 1e-3) / 1e6, 1),
             "unit": "Msamples/s", "ms_per_step": round(wall_ms, 4), "kernel_ms": round(ker_ms, 4),
-            "launches_per_step": mixer.timing().n_launches,
+            "launches_per_step": mixer.timing().n_launches if launches is None else launches,
             "roofline": {"bound": "hbm", "alg_bytes": alg_bytes,
                          "achieved_GBps": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 1),
                          "frac": round(alg_bytes / (ker_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
@@ -263,9 +263,9 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
     s = torch.cuda.current_stream()
     xm.synth(x.data_ptr(), ifmt, SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
     m.set_stream(s.cuda_stream)
+    perm = [(5 * t + 3) % ntr for t in range(ntr)]
     if ptrs:
         # every mix's tracks in a scattered order: no common stride
-        perm = [(5 * t + 3) % ntr for t in range(ntr)]
         ins = [x[b, perm[t]].data_ptr() for b in range(B) for t in range(ntr)]
         outs = [y[b].data_ptr() for b in range(B)]
         step = lambda: m.process_ptrs(ins, outs, B, N)   # noqa: E731
@@ -274,19 +274,27 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
         blk = (N + nb - 1) // nb
         ys = torch.empty((B, F + 64, 2), dtype=y.dtype, device="cuda")
 
+        counts = [0, 0]    # fused / all launches of the last step (timing() covers one call)
+
         def step():
+            counts[:] = [0, 0]
+
+            def tally():
+                counts[0] += m.timing().fast_launches
+                counts[1] += m.timing().n_launches
             m.stream_begin(B)
             got = 0
             for i in range(nb):
                 lo, hi = i * blk, min(N, (i + 1) * blk)
                 got += m.stream_push_strided(x[0, 0, lo:].data_ptr(), N * 2, ntr * N * 2, hi - lo,
                                              ys[0, got:].data_ptr(), (F + 64) * 2, F + 64 - got)
+                tally()
             m.stream_flush_strided(ys[0, got:].data_ptr(), (F + 64) * 2, F + 64 - got)
+            tally()
     else:
         step = lambda: m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)  # noqa: E731
     w, k = timed(step, a.steps, a.warmup, s)
-    fast = m.timing().fast_launches
-    launches = m.timing().n_launches
+    fast, launches = counts if stream else (m.timing().fast_launches, m.timing().n_launches)
 
     def chk():
         from math import gcd
@@ -294,6 +302,8 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
         L, M = fo // g, fi // g
         for b in ends(B):
             xb = x[b].cpu().numpy()                     # [ntr][N][2] (planar: [ntr][2][N] in memory order)
+            if ptrs:
+                xb = xb[perm]                           # slot t of the table holds track perm[t]
             if planar:
                 xb = np.ascontiguousarray(xb.reshape(ntr, 2, N).swapaxes(1, 2))
             if fmt == "s16":
@@ -311,7 +321,7 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
         return True
     report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix"
            + (f", {ofmt} out" if oconv else ""),
-           B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m,
+           B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m, launches=launches,
            kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 

@@ -111,6 +111,7 @@ constexpr size_t BQ_LDS = ((size_t)4 * BQ_KPW * BQ_RP + 64 * (BQ_G + 1)) * 16;  
 
 #ifdef XM_BQ_PROF
 __device__ uint64_t g_bq_prof[4096];   // dev: per-workgroup cycles (compute wave: chunk, barrier wait)
+__device__ uint32_t g_bq_hw[2048];     // dev: HW_ID of each k_biquad_pc wave
 #endif
 
 // The copy wave shared by both biquad kernels: every HBM access of the
@@ -625,63 +626,97 @@ __global__ __launch_bounds__(128) void k_biquad_lane(XmhFxJob j)
 // products sosfilt takes) and hands them to the chain wave through LDS, so
 // the chain wave issues 6 VALU per frame (o = p0 + z0; t = (-a1)*o;
 // t = p1 + t; z0 = z1 + t; u = (-a2)*o; z1 = p2 + u -- bq_mf_pair's order,
-// the same ops as bq_lane_pair bit for bit).  Three waves per workgroup:
+// the same ops as bq_lane_pair bit for bit).  Four waves per workgroup:
 //   chain (wave 0): lane = (clip, section, channel) as k_biquad_lane; section
 //     s filters chunk c = i - 2s - 1 at step i from its product row
 //     P[lane][(i-1) & 1] ([frame][p0 p1 p2], read by ds_read_b128) into its own
 //     planar output row O[lane][i & 1] (ds_write_b128);
 //   producer (wave 1): lane (clip, s, ch) forms the products of chunk i - 2s
 //     into P[lane][i & 1] from section s-1's output row O[lane-4][(i-1) & 1]
-//     (section 0: the interleaved input chunk inb[i & 1]), and the last
-//     section's lanes interleave their chain's previous output row into
-//     outb[i & 1];
-//   copy (wave 2): every HBM access, by per-lane 64-bit addresses: the DMA of
-//     chunk i + 1 (global_load_lds_dwordx4, 4 / C clips per instruction) and
-//     the stores of outb[(i - 1) & 1] (chunk i - 1 - 2 ns).
+//     (section 0: the planar input row PL[i & 1][clip][ch]), 16-B reads all;
+//   load (wave 2): the DMA of chunk i + 2 (global_load_lds_dwordx4 by per-lane
+//     64-bit addresses, 4 / C clips per instruction) into inb[i & 1], waiting
+//     only for chunk i + 1, which it then splits into the planar rows
+//     PL[(i + 1) & 1] -- every chunk has two steps to land;
+//   store (wave 3): the last section's rows O[(i - 1) & 1] (chunk i - 2 ns),
+//     interleaved in registers, to HBM, never waiting for a store.
 // One barrier per step; chunks are 64 frames.  Rows are skewed by 4 floats
-// per lane so the 16-B row accesses of a wave are bank-conflict free.
+// per row so the 16-B row accesses of a wave are bank-conflict free.
 constexpr int PC_CH = 64;                          // frames per chunk (per channel)
 constexpr int PC_KPW = 12;                         // clips per workgroup at most
+#ifndef PC_RA
+#define PC_RA 6                                    // chain: product quads read ahead
+#endif
 constexpr int PC_PS = 2 * PC_CH * 3 + 4;           // floats per lane: P[parity][frame][3] + skew
 constexpr int PC_OS = 2 * PC_CH + 4;               // floats per lane: O[parity][frame] + skew
+constexpr int PC_RS = PC_CH + 4;                   // floats per planar input row + skew
 constexpr int PC_O0 = 64 * PC_PS;                  // O rows (floats); P rows start at 0
-constexpr int PC_IN0 = PC_O0 + 64 * PC_OS;         // inb[parity][clip]: chunks of PC_CH * C floats, contiguous
-constexpr int PC_OUT0 = PC_IN0 + 2 * PC_KPW * PC_CH * 2;   // outb, same layout
-constexpr size_t PC_LDS = (size_t)(PC_OUT0 + 2 * PC_KPW * PC_CH * 2) * 4;   // 157,696 B
+constexpr int PC_IN0 = PC_O0 + 64 * PC_OS;         // inb[chunk & 1][clip]: chunks of PC_CH * C floats, contiguous
+constexpr int PC_PL0 = PC_IN0 + 2 * PC_KPW * PC_CH * 2;   // PL[chunk & 1][clip][ch]: rows of PC_RS floats
+constexpr size_t PC_LDS = (size_t)(PC_PL0 + 2 * PC_KPW * 2 * PC_RS) * 4;   // 158,464 B
 static_assert(PC_LDS <= 160 * 1024, "one workgroup per CU");
-static_assert(PC_PS % 64 == 4 && PC_OS % 64 == 4 && PC_IN0 % 4 == 0, "16-B rows, 4-float skew per lane");
+static_assert(PC_PS % 64 == 4 && PC_OS % 64 == 4 && PC_RS % 64 == 4 && PC_IN0 % 4 == 0 && PC_PL0 % 4 == 0,
+              "16-B rows, 4-float skew per row");
 
+#ifdef XM_BQ_PROF
+// dev: per-wave cycles of k_biquad_pc, [workgroup][wave][work, barrier wait]
+#define PC_PROF_DECL uint64_t pr_[2] = {0, 0}, tq_ = __builtin_amdgcn_s_memtime()
+#define PC_T(n) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pr_[n] += t_ - tq_; tq_ = t_; } while (0)
+#define PC_PROF_OUT(w) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) { \
+    for (int n_ = 0; n_ < 2; ++n_) g_bq_prof[blockIdx.x * 8 + (w) * 2 + n_] = pr_[n_]; \
+    g_bq_hw[blockIdx.x * 4 + (w)] = __builtin_amdgcn_s_getreg(0xF804); } } while (0)
+#else
+#define PC_PROF_DECL do { } while (0)
+#define PC_T(n) do { } while (0)
+#define PC_PROF_OUT(w) do { } while (0)
+#endif
+
+// vmcnt(n) for a wave-uniform n <= 6 (the DMA groups of one chunk)
+__device__ __forceinline__ void pc_vm_wait(int n)
+{
+    switch (n) {
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// The load wave: the DMA of chunk i + 2 into inb[(i + 2) % 3] at step i, so
+// every chunk has two steps to land; only loads are in flight on this wave,
+// and they return in order, so vmcnt(ng) at the end of step i leaves just
+// chunk i + 2's ng DMAs outstanding (chunk i + 1 is in LDS).
 template <int C>
-__device__ __forceinline__ void pc_copy_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, int ns,
-                                             float *lf)
+__device__ __forceinline__ void pc_load_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, float *lf)
 {
     typedef const __attribute__((address_space(1))) float gcf;
-    typedef __attribute__((address_space(1))) float gf;
     typedef __attribute__((address_space(3))) void lds_void;
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int CB = PC_CH * C * 4;              // chunk bytes per clip
     constexpr int LPC = CB / 16;                   // lanes per clip chunk
     constexpr int CPI = 64 / LPC;                  // clips per DMA instruction
     constexpr int NG = PC_KPW / CPI;               // instruction groups at most
+    static_assert(NG <= 6, "pc_vm_wait covers 6 groups");
     const int lane = threadIdx.x & 63;
     const int64_t N = j.frames;
     const int64_t nchunk = (N + PC_CH - 1) / PC_CH, nfull = N / PC_CH;
     const int ng = (nclip + CPI - 1) / CPI;
     const int kl = lane / LPC;                     // this lane's clip within a group
-    uint64_t xa[NG], ya[NG];
+    uint64_t xa[NG];
     const float *xp[NG];
-    float *yp[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
         const int k = min(g * CPI + kl, nclip - 1);   // loads of missing clips fill unused rows
         xp[g] = j.in_ptrs[clip0 + k];
-        yp[g] = j.out_ptrs[clip0 + k];
         xa[g] = (uint64_t)(uintptr_t)xp[g] + (uint64_t)(lane % LPC) * 16u;
-        ya[g] = (uint64_t)(uintptr_t)yp[g] + (uint64_t)(lane % LPC) * 16u;
     }
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)lf);
-    auto load_chunk = [&](int64_t c) __attribute__((always_inline)) {
-        if (c >= nchunk) return;
+    // issue chunk c; returns the DMAs left in flight (0: none, or loaded synchronously)
+    auto load_chunk = [&](int64_t c) __attribute__((always_inline)) -> int {
+        if (c >= nchunk) return 0;
         const int p = (int)(c & 1);
         if (c < nfull) {
 #pragma unroll
@@ -693,9 +728,10 @@ __device__ __forceinline__ void pc_copy_wave(const XmhFxJob &j, int clip0, int n
                              : "s"(m0), "v"(xa[g] + (uint64_t)c * CB)
                              : "memory", "m0");
             }
-            return;
+            return ng;
         }
-        // partial last chunk: element loads with bounds, zero past N
+        // partial last chunk: element loads with bounds, zero past N (the
+        // compiler waits for these before the LDS writes)
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             if (g >= ng) break;
@@ -706,39 +742,112 @@ __device__ __forceinline__ void pc_copy_wave(const XmhFxJob &j, int clip0, int n
                 if (s0 + e < N * C) v[e] = ((gcf *)xp[g])[s0 + e];
             *(f4 *)(lf + PC_IN0 + (p * PC_KPW + g * CPI) * PC_CH * C + lane * 4) = v;
         }
+        return 0;
     };
-    auto store_chunk = [&](int64_t c, int p) __attribute__((always_inline)) {
-        if (c < 0 || c >= nchunk) return;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            if (g >= ng) break;
-            const f4 v = *(const f4 *)(lf + PC_OUT0 + (p * PC_KPW + g * CPI) * PC_CH * C + lane * 4);
-            if (g * CPI + kl >= nclip) continue;   // a clamped lane: not its clip
-            if (c < nfull) {
-                asm volatile("global_store_dwordx4 %0, %1, off" : : "v"(ya[g] + (uint64_t)c * CB), "v"(v) : "memory");
+    // chunk c (landed in inb[c & 1]) -> planar rows PL[c & 1][clip][ch]
+    auto planarize = [&](int64_t c) __attribute__((always_inline)) {
+        if (c >= nchunk) return;
+        const int p = (int)(c & 1);
+        const f4 *ib = (const f4 *)(lf + PC_IN0 + p * PC_KPW * PC_CH * C);
+        float *pl = lf + PC_PL0 + p * PC_KPW * 2 * PC_RS;
+        for (int t = lane; t < nclip * (PC_CH / 4); t += 64) {   // (clip, frame quad)
+            const int k = t / (PC_CH / 4), qd = t % (PC_CH / 4);
+            if (C == 2) {
+                const f4 u = ib[k * (PC_CH / 2) + 2 * qd], v = ib[k * (PC_CH / 2) + 2 * qd + 1];
+                *(f4 *)(pl + (2 * k) * PC_RS + 4 * qd) = f4{u[0], u[2], v[0], v[2]};
+                *(f4 *)(pl + (2 * k + 1) * PC_RS + 4 * qd) = f4{u[1], u[3], v[1], v[3]};
             } else {
-                const int64_t s0 = c * PC_CH * C + (int64_t)(lane % LPC) * 4;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (s0 + e < N * C) ((gf *)yp[g])[s0 + e] = v[e];
+                *(f4 *)(pl + (2 * k) * PC_RS + 4 * qd) = ib[k * (PC_CH / 4) + qd];
             }
         }
     };
     load_chunk(0);
+    load_chunk(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    planarize(0);
+    PC_PROF_DECL;
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        load_chunk(i + 1);
-        store_chunk(i - 1 - 2 * ns, (int)((i - 1) & 1));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // chunk i + 1 landed (and the stores left)
+        PC_T(1);
+        pc_vm_wait(load_chunk(i + 2));             // chunk i + 1 landed (inb[i & 1] was split at step i - 1)
+        planarize(i + 1);
+        PC_T(0);
         __syncthreads();
     }
+    PC_PROF_OUT(2);
+}
+
+// The store wave: at step i the last section's output rows O[(i - 1) & 1]
+// (chunk i - 2 ns) -> interleaved 16-B segments -> HBM; it never waits for a
+// store.
+template <int C>
+__device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, int ns,
+                                              float *lf)
+{
+    typedef __attribute__((address_space(1))) float gf;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    constexpr int CB = PC_CH * C * 4;
+    constexpr int LPC = CB / 16;
+    constexpr int CPI = 64 / LPC;
+    constexpr int NG = PC_KPW / CPI;
+    constexpr int CPG = 4 / C;                     // clips per 4-lane block
+    const int lane = threadIdx.x & 63;
+    const int64_t N = j.frames;
+    const int64_t nchunk = (N + PC_CH - 1) / PC_CH, nfull = N / PC_CH;
+    const int ng = (nclip + CPI - 1) / CPI;
+    const int kl = lane / LPC, sg = lane % LPC;    // clip within a group, 16-B segment within its chunk
+    uint64_t ya[NG];
+    float *yp[NG];
+    int orow[NG];                                  // O row (float offset) of the clip's channel 0
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int k = min(g * CPI + kl, nclip - 1);
+        yp[g] = j.out_ptrs[clip0 + k];
+        ya[g] = (uint64_t)(uintptr_t)yp[g] + (uint64_t)sg * 16u;
+        const int ln = ((k / CPG) * ns + ns - 1) * 4 + (k % CPG) * C;   // the chain lane of (clip, last, ch 0)
+        orow[g] = PC_O0 + ln * PC_OS;
+    }
+    PC_PROF_DECL;
+    __syncthreads();
+    for (int64_t i = 0; i < steps; ++i) {
+        PC_T(1);
+        const int64_t c = i - 2 * ns;
+        if (c >= 0 && c < nchunk) {
+            const int p = (int)((i - 1) & 1);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (g >= ng) break;
+                const float *o = lf + orow[g] + p * PC_CH;
+                f4 v;
+                if (C == 2) {                      // frames 2 sg, 2 sg + 1 of both channels
+                    const f2 a = *(const f2 *)(o + 2 * sg), b = *(const f2 *)(o + PC_OS + 2 * sg);
+                    v = f4{a[0], b[0], a[1], b[1]};
+                } else {
+                    v = *(const f4 *)(o + 4 * sg);
+                }
+                if (g * CPI + kl >= nclip) continue;   // a clamped lane: not its clip
+                if (c < nfull) {
+                    asm volatile("global_store_dwordx4 %0, %1, off" : : "v"(ya[g] + (uint64_t)c * CB), "v"(v) : "memory");
+                } else {
+                    const int64_t s0 = c * PC_CH * C + (int64_t)sg * 4;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (s0 + e < N * C) ((gf *)yp[g])[s0 + e] = v[e];
+                }
+            }
+        }
+        PC_T(0);
+        __syncthreads();
+    }
+    PC_PROF_OUT(3);
 }
 
 template <int C, bool ST>
-__global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
+__global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
 {
     typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
     constexpr int CPG = 4 / C;                     // clips per group (a block of 4 lanes)
     extern __shared__ bq_f4 bq_lds[];
     float *lf = (float *)bq_lds;
@@ -752,7 +861,11 @@ __global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
     const int64_t steps = nchunk + 2 * ns + 1;
     const int wave = threadIdx.x >> 6;
     if (wave == 2) {
-        pc_copy_wave<C>(j, clip0, nclip, steps, ns, lf);
+        pc_load_wave<C>(j, clip0, nclip, steps, lf);
+        return;
+    }
+    if (wave == 3) {
+        pc_store_wave<C>(j, clip0, nclip, steps, ns, lf);
         return;
     }
     const int lane = threadIdx.x & 63;
@@ -766,47 +879,34 @@ __global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
 
     if (wave == 1) {
         // ---------------- producer: products one step ahead ------------------
-        const bool last = valid && s == ns - 1;
         const int kq = valid ? kk : 0;
+        PC_PROF_DECL;
         __syncthreads();
         for (int64_t i = 0; i < steps; ++i) {
+            PC_T(1);
             const int par = (int)(i & 1);
-            // source of chunk i - 2s: section s - 1's output row, or the input
-            int src, stride;
-            if (valid && s == 0) {
-                src = PC_IN0 + (par * PC_KPW + kq) * PC_CH * C + ch;
-                stride = C;
-            } else {
-                src = (valid ? O_lane - 4 * PC_OS : O_lane) + (par ^ 1) * PC_CH;   // lane - 4 = section s - 1
-                stride = 1;
-            }
+            // chunk i - 2s: section s - 1's output row, or the planar input row
+            const float *src = valid && s == 0 ? lf + PC_PL0 + ((par * PC_KPW + kq) * 2 + ch) * PC_RS
+                                               : lf + (valid ? O_lane - 4 * PC_OS : O_lane) + (par ^ 1) * PC_CH;
             float *Pw = lf + P_lane + par * PC_CH * 3;
-#pragma unroll 4
+            // the whole source row first: the compiler cannot move these reads
+            // past the product writes (same LDS array), and one read per quad
+            // would expose the LDS latency 16 times a step
+            f4 xr[PC_CH / 4];
+#pragma unroll
+            for (int qd = 0; qd < PC_CH / 4; ++qd) xr[qd] = ((const f4 *)src)[qd];
+#pragma unroll
             for (int qd = 0; qd < PC_CH / 4; ++qd) {
-                float x[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) x[e] = lf[src + (4 * qd + e) * stride];
-                f4 w0, w1, w2;
-                w0 = f4{b0 * x[0], b1 * x[0], b2 * x[0], b0 * x[1]};
-                w1 = f4{b1 * x[1], b2 * x[1], b0 * x[2], b1 * x[2]};
-                w2 = f4{b2 * x[2], b0 * x[3], b1 * x[3], b2 * x[3]};
+                const f4 x = xr[qd];
                 f4 *pw = (f4 *)(Pw + 12 * qd);
-                pw[0] = w0;
-                pw[1] = w1;
-                pw[2] = w2;
+                pw[0] = f4{b1 * x[0], b2 * x[0], b1 * x[1], b2 * x[1]};
+                pw[1] = f4{b1 * x[2], b2 * x[2], b1 * x[3], b2 * x[3]};
+                pw[2] = f4{b0 * x[0], b0 * x[1], b0 * x[2], b0 * x[3]};
             }
-            if (last) {   // the last section's previous output -> outb[i & 1], interleaved
-                const f4 *Or = (const f4 *)(lf + O_lane + (par ^ 1) * PC_CH);
-                float *ob = lf + PC_OUT0 + (par * PC_KPW + kq) * PC_CH * C + ch;
-#pragma unroll 4
-                for (int qd = 0; qd < PC_CH / 4; ++qd) {
-                    const f4 v = Or[qd];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) ob[(4 * qd + e) * C] = v[e];
-                }
-            }
+            PC_T(0);
             __syncthreads();
         }
+        PC_PROF_OUT(1);
         return;
     }
 
@@ -818,8 +918,10 @@ __global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
         z0 = st[ch];
         z1 = st[C + ch];
     }
+    PC_PROF_DECL;
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
+        PC_T(1);
         const int64_t c = i - 2 * s - 1;           // chunk this lane filters
         const bool act = valid && c >= 0 && c < nchunk;
         const float z0s = z0, z1s = z1;
@@ -831,7 +933,8 @@ __global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
             // a streamed block's last chunk: frames past N are padding and must
             // not advance the state (wave-uniform branch)
             for (int f = 0; f < PC_CH; ++f) {
-                const float p0 = Pr[3 * f], p1 = Pr[3 * f + 1], p2 = Pr[3 * f + 2];
+                const float *q = Pr + 12 * (f >> 2);
+                const float p0 = q[8 + (f & 3)], p1 = q[2 * (f & 3)], p2 = q[2 * (f & 3) + 1];
                 const float o = p0 + z0;
                 if (!(tail && c * PC_CH + f >= N)) {
                     z0 = z1 + (p1 + na1 * o);
@@ -840,31 +943,44 @@ __global__ __launch_bounds__(192) void k_biquad_pc(XmhFxJob j)
                 Ow[f] = o;
             }
         } else {
-            // quads of 4 frames (12 products = 3 x 16 B), read two quads ahead
+            // quads of 4 frames (12 products = 3 x 16 B: (p1, p2) of frames
+            // 0-1, of frames 2-3, p0 of frames 0-3), read PC_RA quads ahead.
+            // Per frame 4 instructions on the 4-op dependence: o = p0 + z0;
+            // (t, u) = (-a1, -a2) * o (v_pk_mul_f32); (t, z1') = (p1, p2) +
+            // (t, u) (v_pk_add_f32); z0 = z1 + t -- each half the very
+            // operation bq_mf_pair issues
             const f4 *P4 = (const f4 *)Pr;
-            f4 A0 = P4[0], A1 = P4[1], A2 = P4[2];
-            f4 B0 = P4[3], B1 = P4[4], B2 = P4[5];
+            const f2 nA = f2{na1, na2};
+            f4 R[PC_CH / 4][3];
+#pragma unroll
+            for (int qd = 0; qd < PC_RA; ++qd)
+#pragma unroll
+                for (int e = 0; e < 3; ++e) R[qd][e] = P4[3 * qd + e];
 #pragma unroll
             for (int qd = 0; qd < PC_CH / 4; ++qd) {
-                f4 N0, N1, N2;
-                if (qd + 2 < PC_CH / 4) {
-                    N0 = P4[3 * (qd + 2)];
-                    N1 = P4[3 * (qd + 2) + 1];
-                    N2 = P4[3 * (qd + 2) + 2];
+                if (qd + PC_RA < PC_CH / 4) {
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) R[qd + PC_RA][e] = P4[3 * (qd + PC_RA) + e];
                 }
-                const float pa[4] = {A0[0], A0[1], A0[2], 0.0f}, pb[4] = {A0[3], A1[0], A1[1], 0.0f};
-                const float pc[4] = {A1[2], A1[3], A2[0], 0.0f}, pd[4] = {A2[1], A2[2], A2[3], 0.0f};
                 float o[4];
-                bq_mf_pair(pa, pb, z0, z1, na1, na2, o[0], o[1]);
-                bq_mf_pair(pc, pd, z0, z1, na1, na2, o[2], o[3]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const f4 &Q = R[qd][e >> 1];
+                    const f2 p12 = (e & 1) ? f2{Q[2], Q[3]} : f2{Q[0], Q[1]};
+                    o[e] = R[qd][2][e] + z0;
+                    const f2 tu = nA * f2{o[e], o[e]};
+                    const f2 r = p12 + tu;
+                    z0 = z1 + r.x;
+                    z1 = r.y;
+                }
                 ((f4 *)Ow)[qd] = f4{o[0], o[1], o[2], o[3]};
-                A0 = B0; A1 = B1; A2 = B2;
-                if (qd + 2 < PC_CH / 4) { B0 = N0; B1 = N1; B2 = N2; }
             }
         }
         if (!act) { z0 = z0s; z1 = z1s; }
+        PC_T(0);
         __syncthreads();                           // products of step i + 1 ready; outputs visible
     }
+    PC_PROF_OUT(0);
     if (ST && st) {
         st[ch] = z0;
         st[C + ch] = z1;
@@ -1045,7 +1161,12 @@ __global__ __launch_bounds__(64 * FR_WAVES) void k_fir_rb(XmhFxJob j)
         for (int i = 0; i < 2 * FR_U; ++i) hc[i] = hn[i];
     }
     if (tb + FR_U <= K) {                          // one more whole block: then the window is B ++ next
-        block(A, B, hc);
+        // (hc was loaded with a clamped block start here: the taps come
+        // straight from h)
+        float hl[FR_U];
+#pragma unroll
+        for (int t = 0; t < FR_U; ++t) hl[t] = h[K - 1 - (tb + t)];
+        block(A, B, hl);
 #pragma unroll
         for (int u = 0; u < FR_U; ++u) {
             A[u] = B[u];
@@ -1161,7 +1282,7 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
         const int kpw = std::min(16 / j->n_sos * (4 / j->channels), PC_KPW);
         if (xmh_func_lds((const void *)pk, (int)PC_LDS)) return -1001;   // once per (kernel, device)
         XmhFxJob jj = *j;
-        hipLaunchKernelGGL(pk, dim3((unsigned)((j->n_clips + kpw - 1) / kpw)), dim3(192), PC_LDS,
+        hipLaunchKernelGGL(pk, dim3((unsigned)((j->n_clips + kpw - 1) / kpw)), dim3(256), PC_LDS,
                            (hipStream_t)stream, jj);
         return hipGetLastError() == hipSuccess ? 0 : -1001;
     }
@@ -1182,6 +1303,10 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
 extern "C" __attribute__((visibility("default"))) int xmh_dev_bq_prof(uint64_t *host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_prof), sizeof(g_bq_prof)) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int xmh_dev_bq_hw(uint32_t *host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_hw), sizeof(g_bq_hw)) == hipSuccess ? 0 : -1;
 }
 #endif
 
