@@ -14,7 +14,7 @@ Headline-shaped C-API variants (512 mixes x 8 stereo tracks x ~10 s, gain
 ramps, the kernel each one lands on in "kernel"):
 odd     frames_in 480001 (fused kernel, odd-length path)
 ptrs    irregular pointer table (tracks in scattered order: generic kernel)
-up      44.1k -> 48k fp32 (generic kernel)
+up      44.1k -> 48k fp32 (fused kernel, UP)
 s16rs   48k -> 44.1k s16 Q15 (fused kernel, IO 2)
 planar  48k -> 44.1k fp32, planar tracks and mixes (fused kernel, PL)
 conv    48k -> 44.1k, s16 tracks into the fp32 mix (fused kernel, IO 1)

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Writes csrc/xm_pk_taps.h: the packed-tap asm blocks of the fast kernel
-(csrc/xm_resample_fast.hip, TAPS == 2), one block per 8-tap coefficient group.
+(csrc/xm_resample_fast.hip, TAPS == 2), one block per 8-tap coefficient group
+(G0, G1: 8 taps; G2: the 6-tap last group of 48k->44.1k, G2T5 / G2T4: the 5- and
+4-tap last groups of 44.1k->48k).
 
 Operands of every block: %0..%3 product temps (=&v), %4 a0, %5 a1 (+v, the
 (L, R) accumulators of outputs k, k+1), %6..%13 coefficient SGPR pairs
@@ -134,7 +136,7 @@ for n in range(1, 5):
     for first in (True, False):
         for two in (True, False):
             out.append(f'#define XM_V2_{"F" if first else "R"}{n}_{"TWO" if two else "ONE"} "{vblock(n, first, two)}"')
-for first, n, name in ((True, 8, "G0"), (False, 8, "G1"), (False, 6, "G2")):
+for first, n, name in ((True, 8, "G0"), (False, 8, "G1"), (False, 6, "G2"), (False, 5, "G2T5"), (False, 4, "G2T4")):
     for two in (True, False):
         out.append(f'#define XM_PK_{name}_{"TWO" if two else "ONE"} "{block(n, first, two)}"')
 for n in (2, 4):
