@@ -1,9 +1,10 @@
 #!/bin/bash
-# Dev (GPU box, repo root): PMC passes over one effects config line of
-# tools/bench_configs.py (fir or bq): where the kernel's wave time goes and its
+# Dev (GPU box, repo root): PMC passes over one config line of
+# tools/bench_configs.py (fir, bq, up, ...; "bench": the headline bench.py
+# command): where the kernel's wave time goes and its
 # HBM bytes (FETCH_SIZE and WRITE_SIZE in passes of their own, never with a
 # tracing domain).  Per-launch averages of the kernels whose name matches.
-#   tools/pmc_fx.sh <tag> <fir|bq> <kernel-name-substring>
+#   tools/pmc_fx.sh <tag> <fir|bq|up|...|bench> <kernel-name-substring>
 set -o pipefail
 TAG=${1:-fx}; CFG=${2:-fir}; KN=${3:-k_fir_rb}
 OUT=gpurun_out/$TAG
@@ -15,7 +16,11 @@ P3="FETCH_SIZE"
 P4="WRITE_SIZE"
 for k in 1 2 3 4; do
   eval C=\$P$k
-  timeout -s KILL 120 rocprofv3 --pmc $C -d $OUT/p$k -o run --output-format csv -- python3 tools/bench_configs.py $CFG --steps 2 --warmup 1 --no-check > $OUT/p$k.log 2>&1 || { tail -5 $OUT/p$k.log; exit 1; }
+  if [ "$CFG" = bench ]; then
+    timeout -s KILL 120 rocprofv3 --pmc $C -d $OUT/p$k -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-check > $OUT/p$k.log 2>&1 || { tail -5 $OUT/p$k.log; exit 1; }
+  else
+    timeout -s KILL 120 rocprofv3 --pmc $C -d $OUT/p$k -o run --output-format csv -- python3 tools/bench_configs.py $CFG --steps 2 --warmup 1 --no-check > $OUT/p$k.log 2>&1 || { tail -5 $OUT/p$k.log; exit 1; }
+  fi
   python3 - $OUT/p$k/run_counter_collection.csv "$KN" <<'PY'
 import csv, sys, collections
 per = collections.defaultdict(lambda: collections.defaultdict(float))
