@@ -80,14 +80,50 @@ def test_fast_split_odd_lengths(xm, gpu, N):
         assert bits_equal(got[b], CO.resample_f32(xs[b], 147, 160)), b
 
 
+@pytest.mark.parametrize("N", [48000, 48001])
+def test_fast_kernel_pointer_tables_4gb_apart(xm, gpu, N):
+    """Tracks of one mix 4.5 GB apart (the two ends of one 4.6 GB tensor) and
+    mixes mixing near and far tracks: the FAR kernel (a 64-bit base per track
+    row), bit-exact, fast_launches == 1; 5 mixes leave padding waves."""
+    import torch
+    from bench import RAMPS, SEED
+    B = 5
+    fl = 2 * N
+    big = torch.empty(4_600_000_000 // 4, dtype=torch.float32, device="cuda")
+    # track t of mix b at the low end for even t, the high end for odd t
+    lo = [b * 8 * fl + t * fl for b in range(B) for t in range(8)]
+    hi = [big.numel() - (1 + b * 8 + t) * fl for b in range(B) for t in range(8)]
+    offs = [lo[i] if i % 2 == 0 else hi[i] for i in range(B * 8)]
+    offs[3 * 8 + 5] = lo[3 * 8 + 5]   # mix 3: one more low track
+    for i, o in enumerate(offs):
+        xm.synth(big[o:].data_ptr(), "f32", SEED, 900 + i, 1, 2, N)
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks(RAMPS)
+    F = m.out_frames(N)
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    m.process_ptrs([big[o:].data_ptr() for o in offs], [y[b].data_ptr() for b in range(B)], B, N)
+    torch.cuda.synchronize()
+    t = m.timing()
+    assert t.n_launches == 1 and t.fast_launches == 1, (t.n_launches, t.fast_launches)
+    assert (max(offs) - min(offs)) * 4 > 4 << 30
+    got = y.cpu().numpy()
+    for b in range(B):
+        tracks = [big[offs[b * 8 + t]: offs[b * 8 + t] + fl].view(N, 2).cpu().numpy() for t in range(8)]
+        assert bits_equal(got[b], CO.resample_mix_f32(tracks, RAMPS, 147, 160)), b
+    del big
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("own_alloc", [False, True])
 @pytest.mark.parametrize("N", [48000, 48001])
 def test_fast_kernel_pointer_tables(xm, gpu, N, own_alloc):
     """Irregular per-track pointer tables stay on the fused kernel (one
     buffer resource per mix based at its lowest track, per-track offsets
-    from the table): tracks in scattered order inside one tensor, plus (with
-    own_alloc) one mix whose tracks are separate allocations; outputs through
-    a table too."""
+    from the table; a mix whose tracks span 2 GB or more runs the FAR
+    kernel, one resource per track): tracks in scattered order inside one
+    tensor, plus (with own_alloc) one mix whose tracks are separate
+    allocations; outputs through a table too."""
     import torch
     from bench import RAMPS, SEED
     B = 4
@@ -105,12 +141,7 @@ def test_fast_kernel_pointer_tables(xm, gpu, N, own_alloc):
     m.process_ptrs(ins, outs, B, N)
     torch.cuda.synchronize()
     t = m.timing()
-    # the launcher takes a table when every mix's 8 tracks lie within 2 GB
-    # (one 32-bit buffer resource per mix); where the caching allocator put
-    # the separately allocated tracks decides that for the last mix
-    own_p = [o.data_ptr() for o in own]
-    fits = max(own_p) - min(own_p) + (N + 32) * 8 < 1 << 31
-    assert t.fast_launches == int(fits), (t.n_launches, t.fast_launches, fits)
+    assert t.n_launches == 1 and t.fast_launches == 1, (t.n_launches, t.fast_launches)
     xs = x.cpu().numpy()
     got = y.cpu().numpy()
     for b in range(B):

@@ -13,12 +13,13 @@ c5  config 5 on this GPU: 512 mixes x 8 of their 64 s16 tracks -> int32 partial
 Headline-shaped C-API variants (512 mixes x 8 stereo tracks x ~10 s, gain
 ramps, the kernel each one lands on in "kernel"):
 odd     frames_in 480001 (fused kernel, odd-length path)
-ptrs    irregular pointer table (tracks in scattered order: generic kernel)
+ptrs    irregular pointer table (tracks in scattered order: fused kernel)
 up      44.1k -> 48k fp32 (fused kernel, UP)
+far     headline through a pointer table whose mixes' tracks lie ~7.9 GB apart (FAR kernel)
 s16rs   48k -> 44.1k s16 Q15 (fused kernel, IO 2)
 planar  48k -> 44.1k fp32, planar tracks and mixes (fused kernel, PL)
 conv    48k -> 44.1k, s16 tracks into the fp32 mix (fused kernel, IO 1)
-stream  the headline pushed in 8 blocks through stream_push (fused bulk + generic heads)
+stream  the headline pushed in 8 blocks through stream_push (fused bulk straight from the block + generic heads)
 oconv   the headline with XM_MIXER_OUT_CONVERT: s16 output (fused kernel epilogue)
 Unit: input samples (frames x channels x tracks) per second; roofline
 fraction = algorithmic bytes (inputs once + output once) / kernel time / 8 TB/s.
@@ -249,7 +250,7 @@ def c5(a):
 
 
 def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=False, conv=False,
-           stream=False, oconv=False):
+           stream=False, oconv=False, far=False):
     B, ntr = a.mixes, 8
     m = xm.Mixer(fi, fo, 2, fmt, mem="device", planar=planar, convert_in=conv, convert_out=oconv)
     m.set_tracks(Q15_RAMPS if fmt == "s16" else RAMPS)
@@ -264,7 +265,16 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
     xm.synth(x.data_ptr(), ifmt, SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
     m.set_stream(s.cuda_stream)
     perm = [(5 * t + 3) % ntr for t in range(ntr)]
-    if ptrs:
+    half = B * ntr // 2
+    fidx = lambda b, t: (b * ntr + t) // 2 + (half if t % 2 else 0)   # noqa: E731
+    if far:
+        # even tracks of every mix from the first half of the batch tensor,
+        # odd ones from the second: a mix's tracks lie ~7.9 GB apart (FAR kernel)
+        xf_ = x.view(B * ntr, N, 2)
+        ins = [xf_[fidx(b, t)].data_ptr() for b in range(B) for t in range(ntr)]
+        outs = [y[b].data_ptr() for b in range(B)]
+        step = lambda: m.process_ptrs(ins, outs, B, N)   # noqa: E731
+    elif ptrs:
         # every mix's tracks in a scattered order: no common stride
         ins = [x[b, perm[t]].data_ptr() for b in range(B) for t in range(ntr)]
         outs = [y[b].data_ptr() for b in range(B)]
@@ -302,7 +312,9 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
         L, M = fo // g, fi // g
         for b in ends(B):
             xb = x[b].cpu().numpy()                     # [ntr][N][2] (planar: [ntr][2][N] in memory order)
-            if ptrs:
+            if far:
+                xb = np.stack([x.view(B * ntr, N, 2)[fidx(b, t)].cpu().numpy() for t in range(ntr)])
+            elif ptrs:
                 xb = xb[perm]                           # slot t of the table holds track perm[t]
             if planar:
                 xb = np.ascontiguousarray(xb.reshape(ntr, 2, N).swapaxes(1, 2))
@@ -328,6 +340,7 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
 
 def odd(a): _shape(a, "odd", N=480001)
 def ptrs(a): _shape(a, "ptrs", ptrs=True)
+def far(a): _shape(a, "far", far=True)
 def up(a): _shape(a, "up", fi=44100, fo=48000, N=441000)
 def s16rs(a): _shape(a, "s16rs", fmt="s16")
 def planar(a): _shape(a, "planar", planar=True)
