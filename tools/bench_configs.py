@@ -163,8 +163,14 @@ def c4(a):
 
 def fir(a):
     """FIR effect alone: K-tap filter over 1024 stereo 10 s clips @ 44.1 kHz,
-    device memory, out of place (k_fir_rb)."""
-    B, N, K = a.clips_fx, 441000, a.fir_k
+    device memory, out of place (k_fir_rb); one line per K of --fir-k."""
+    for K in [int(k) for k in str(a.fir_k).split(",")]:
+        _fir(a, K)
+        torch.cuda.empty_cache()
+
+
+def _fir(a, K):
+    B, N = a.clips_fx, 441000
     h = (np.sin(np.arange(K, dtype=np.float64) * 0.37) / (1 + np.arange(K))).astype(np.float32)
     e = xm.Effects(44100, 2, mem="device")
     e.add_fir(h)
@@ -177,7 +183,7 @@ def fir(a):
     w, k = timed(lambda: e.process_ptrs(ins, outs, N), a.steps, a.warmup, s)
     ok = parity(a, lambda: all(beq(y[b].cpu().numpy(), CO.fir_f32(x[b].cpu().numpy(), h)) for b in ends(B)))
     alg = 2 * B * N * 2 * 4
-    line = {"config": "fir", "workload": f"{K}-tap FIR (upfirdn order), {B} stereo 10 s fp32 clips @ 44.1 kHz",
+    line = {"config": "fir" if K == 63 else f"fir{K}", "taps": K, "workload": f"{K}-tap FIR (upfirdn order), {B} stereo 10 s fp32 clips @ 44.1 kHz",
             "value": round(B * N * 2 / (w * 1e-3) / 1e6, 1), "unit": "Msamples/s", "ms_per_step": round(w, 4),
             "kernel_ms": round(k, 4),
             "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved_GBps": round(alg / (k * 1e-3) / 1e9, 1),
@@ -361,7 +367,7 @@ def main():
     ap.add_argument("--mixes", type=int, default=512, help="headline-shaped variants")
     ap.add_argument("--no-check", action="store_true", help="skip the post-timing oracle checks")
     ap.add_argument("--clips-fx", type=int, default=1024, help="fir / bq: clips")
-    ap.add_argument("--fir-k", type=int, default=63, help="fir: taps")
+    ap.add_argument("--fir-k", default="63", help="fir: taps (a comma list: one line each)")
     a = ap.parse_args()
     for w in a.which:
         globals()[w](a)
