@@ -962,6 +962,31 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
 #pragma unroll
                     for (int e = 0; e < 3; ++e) R[qd + PC_RA][e] = P4[3 * (qd + PC_RA) + e];
                 }
+#ifdef XM_BQ_PC_ASM
+                // o of frames (0, 1) and (2, 3) built in place as register
+                // pairs: the product (t, u) broadcasts o from the pair's low
+                // or high half by op_sel, so no o is copied into the store
+                // pair (the compiler's form moved every odd frame's o)
+                f2 op[2];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const f4 &Q = R[qd][e >> 1];
+                    const f2 p12 = (e & 1) ? f2{Q[2], Q[3]} : f2{Q[0], Q[1]};
+                    f2 &oo = op[e >> 1];
+                    f2 tu;
+                    if (e & 1) {
+                        oo.y = R[qd][2][e] + z0;
+                        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(tu) : "v"(nA), "v"(oo));
+                    } else {
+                        oo.x = R[qd][2][e] + z0;
+                        asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(tu) : "v"(nA), "v"(oo));
+                    }
+                    const f2 r = p12 + tu;
+                    z0 = z1 + r.x;
+                    z1 = r.y;
+                }
+                ((f4 *)Ow)[qd] = f4{op[0].x, op[0].y, op[1].x, op[1].y};
+#else
                 float o[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -974,6 +999,7 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
                     z1 = r.y;
                 }
                 ((f4 *)Ow)[qd] = f4{o[0], o[1], o[2], o[3]};
+#endif
             }
         }
         if (!act) { z0 = z0s; z1 = z1s; }
@@ -1186,6 +1212,19 @@ __global__ __launch_bounds__(64 * FR_WAVES) void k_fir_rb(XmhFxJob j)
             acc[u] = acc[u] + xv * hv;
         }
     }
+#ifdef XM_FIR_DIRECT_OUT
+    // a whole tile inside the clip with 8-B aligned frames: each lane stores
+    // its 7 consecutive output frames straight from registers (immediate
+    // offsets from one address; the 7 stores of a wave fill every byte of its
+    // 3.5 KB, so the L2 merges them into whole lines) -- no LDS round trip,
+    // no second barrier, no per-chunk bounds arithmetic
+    if (n0 + FR_TILE <= N && (C == 1 || ((uintptr_t)y & 7) == 0)) {   // uniform per workgroup
+        V *yl = (V *)(y + (n0 + base) * C);
+#pragma unroll
+        for (int u = 0; u < FR_U; ++u) yl[u] = acc[u];
+        return;
+    }
+#endif
     // outputs -> wave-private LDS (after the whole workgroup is done with the
     // tile) -> whole 16-B chunks in frame order
     __syncthreads();
