@@ -962,7 +962,7 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
 #pragma unroll
                     for (int e = 0; e < 3; ++e) R[qd + PC_RA][e] = P4[3 * (qd + PC_RA) + e];
                 }
-#ifdef XM_BQ_PC_ASM
+#ifndef XM_BQ_PC_CXX   // dev A/B: -DXM_BQ_PC_CXX, the compiler-scheduled form (7.72-7.74 ms vs 7.32-7.33 on one box)
                 // o of frames (0, 1) and (2, 3) built in place as register
                 // pairs: the product (t, u) broadcasts o from the pair's low
                 // or high half by op_sel, so no o is copied into the store
@@ -1212,19 +1212,9 @@ __global__ __launch_bounds__(64 * FR_WAVES) void k_fir_rb(XmhFxJob j)
             acc[u] = acc[u] + xv * hv;
         }
     }
-#ifdef XM_FIR_DIRECT_OUT
-    // a whole tile inside the clip with 8-B aligned frames: each lane stores
-    // its 7 consecutive output frames straight from registers (immediate
-    // offsets from one address; the 7 stores of a wave fill every byte of its
-    // 3.5 KB, so the L2 merges them into whole lines) -- no LDS round trip,
-    // no second barrier, no per-chunk bounds arithmetic
-    if (n0 + FR_TILE <= N && (C == 1 || ((uintptr_t)y & 7) == 0)) {   // uniform per workgroup
-        V *yl = (V *)(y + (n0 + base) * C);
-#pragma unroll
-        for (int u = 0; u < FR_U; ++u) yl[u] = acc[u];
-        return;
-    }
-#endif
+    // (measured and dropped: storing whole aligned tiles straight from the
+    // registers, 7 x 8-B frames per lane, saved 1.5 % at K = 63 but cost 22 %
+    // at K = 15, where the partial-line writes set the pace)
     // outputs -> wave-private LDS (after the whole workgroup is done with the
     // tile) -> whole 16-B chunks in frame order
     __syncthreads();

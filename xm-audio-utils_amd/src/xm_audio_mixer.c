@@ -1063,6 +1063,8 @@ int xm_audio_mixer_stream_flush(XmAudioMixer *m, void *out, ptrdiff_t out_mix_st
  * per-track resample bit for bit: 0 + 1*r == r, and a Q15 unity term is the
  * sample itself), then placed at its output-frame offset and mixed with the
  * gains evaluated at the mix's output frame. */
+static const XmhGain k_unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
+
 static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrackPlacement *place,
                            void *const *out, size_t batch, size_t out_frames)
 {
@@ -1101,7 +1103,6 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
     const void *const *din = NULL;
     void *const *dout = NULL;
     rc = ptr_table(m, hp, 2 * nb, out, batch, &din, &dout);
-    free(hp);
     if (!rc) rc = xmh_memcpy_h2d(m->place_dev, pl, sizeof(int64_t) * 2 * (size_t)ntr, m->stream);
     if (!rc) rc = xmh_event_record(m->ev[2], m->stream);
     for (int tr = 0; !rc && tr < ntr; ++tr) {
@@ -1116,18 +1117,21 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
         j.frames_in = place[tr].frames_in;
         j.frames_out = pl[2 * tr + 1];
         j.in_ptrs = din + (size_t)tr * batch;
+        j.in_ptrs_host = (const void *const *)hp + (size_t)tr * batch;   /* the fused kernel's admission checks */
         j.out = (char *)m->d_fx + off[tr];
         j.out_mix_stride = pl[2 * tr + 1] * C;
         j.gains = m->unity_dev;
+        j.gains_host = &k_unity_gain;
         j.unity = 1;
         j.rs.L = t->d.L;
         j.rs.M = t->d.M;
         j.rs.T = t->d.T;
         j.rs.rm = t->d.rm;
         j.rs.H = t->H_dev;
-        j.rs.fast = 0;
+        j.rs.fast = t->fast;   /* 48k <-> 44.1k stereo f32 tracks: the fused kernel's 1-track rows */
         rc = xmh_launch_mix(&j, m->stream, &launches, &m->timing.fast_launches);
     }
+    free(hp);
     if (!rc) {
         XmhMixJob j;
         memset(&j, 0, sizeof j);
