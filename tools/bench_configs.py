@@ -16,6 +16,8 @@ odd     frames_in 480001 (fused kernel, odd-length path)
 ptrs    irregular pointer table (tracks in scattered order: fused kernel)
 up      44.1k -> 48k fp32 (fused kernel, UP)
 far     headline through a pointer table whose mixes' tracks lie ~7.9 GB apart (FAR kernel)
+mono8   1024 mixes x 8 mono f32 tracks, 48k -> 44.1k (the headline's input bytes; MONO kernel)
+mono1   8192 mono 10 s f32 clips 44.1k -> 48k at unity gain (config 1's shape, batched; MONO kernel)
 s16rs   48k -> 44.1k s16 Q15 (fused kernel, IO 2)
 planar  48k -> 44.1k fp32, planar tracks and mixes (fused kernel, PL)
 conv    48k -> 44.1k, s16 tracks into the fp32 mix (fused kernel, IO 1)
@@ -344,6 +346,38 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
            parity_check=parity(a, chk))
 
 
+def _mono(a, name, ntr, B, fi, fo, N):
+    """Mono f32 on the fused kernel (MONO): B mixes x ntr mono tracks."""
+    m = xm.Mixer(fi, fo, 1, "f32", mem="device")
+    ramps = RAMPS[:ntr] if ntr > 1 else [dict(gain0=1.0)]
+    m.set_tracks(ramps)
+    F = m.out_frames(N)
+    x = torch.empty((B, ntr, N), dtype=torch.float32, device="cuda")
+    y = torch.empty((B, F), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B * ntr, 1, N, 0, s.cuda_stream)
+    m.set_stream(s.cuda_stream)
+    w, k = timed(lambda: m.process_strided(x.data_ptr(), N, ntr * N, y.data_ptr(), F, B, N), a.steps, a.warmup, s)
+    fast, launches = m.timing().fast_launches, m.timing().n_launches
+
+    def chk():
+        from math import gcd
+        g = gcd(fi, fo)
+        L, M = fo // g, fi // g
+        for b in ends(B):
+            xb = x[b].cpu().numpy()[:, :, None]         # [ntr][N][1]
+            want = CO.resample_mix_f32(list(xb), ramps, L, M)
+            if not beq(y[b].cpu().numpy()[:, None], want):
+                return False
+        return True
+    report(name, f"{name}: {B} mixes x {ntr} mono f32 tracks x {N} frames, {fi}->{fo} f32 mix",
+           B * ntr * N, B * ntr * N * 4 + B * F * 4, w, k, m, launches=launches,
+           kernel="k_rs147_mix MONO" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
+           parity_check=parity(a, chk))
+
+
+def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)
+def mono1(a): _mono(a, "mono1", 1, 16 * a.mixes, 44100, 48000, 441000)
 def odd(a): _shape(a, "odd", N=480001)
 def ptrs(a): _shape(a, "ptrs", ptrs=True)
 def far(a): _shape(a, "far", far=True)
