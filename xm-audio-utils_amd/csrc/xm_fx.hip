@@ -860,11 +860,20 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
     const int64_t nchunk = (N + PC_CH - 1) / PC_CH;
     const int64_t steps = nchunk + 2 * ns + 1;
     const int wave = threadIdx.x >> 6;
-    if (wave == 2) {
+    // the store wave (LDS reads only) as wave 2: a workgroup's waves take the
+    // SIMDs in the cyclic order 0, 2, 1, 3, so wave 2 shares the chain wave's
+    // half of the LDS store path, which the load wave's writes no longer
+    // contend for (7.36 -> 7.26-7.29 ms same box; dev A/B: -DXM_BQ_PC_NOSWAP)
+#ifdef XM_BQ_PC_NOSWAP
+    constexpr int W_LOAD = 2, W_STORE = 3;
+#else
+    constexpr int W_LOAD = 3, W_STORE = 2;
+#endif
+    if (wave == W_LOAD) {
         pc_load_wave<C>(j, clip0, nclip, steps, lf);
         return;
     }
-    if (wave == 3) {
+    if (wave == W_STORE) {
         pc_store_wave<C>(j, clip0, nclip, steps, ns, lf);
         return;
     }
