@@ -1,6 +1,6 @@
 #!/bin/bash
 # Dev (GPU box): mono tests on the product lib, then the mono lines A (lib:
-# paired-round whole-segment stores) / B (lib_ab: -DXM_AB_NO_MPAIR) with a
+# the store variant under test) / B (lib_ab: the A/B macro it was built with) with a
 # WRITE_SIZE pass each.
 mkdir -p gpurun_out/mpab
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fast_mono.py tests/test_gpu_fast_up.py -x -q --timeout 120 --timeout-method thread > gpurun_out/mpab/pytest.log 2>&1 || { tail -30 gpurun_out/mpab/pytest.log; exit 1; }
