@@ -18,6 +18,7 @@ up      44.1k -> 48k fp32 (fused kernel, UP)
 far     headline through a pointer table whose mixes' tracks lie ~7.9 GB apart (FAR kernel)
 mono8   1024 mixes x 8 mono f32 tracks, 48k -> 44.1k (the headline's input bytes; MONO kernel)
 mono1   8192 mono 10 s f32 clips 44.1k -> 48k at unity gain (config 1's shape, batched; MONO kernel)
+c1s16   the same in config 1's own s16 form (generic kernel)
 s16rs   48k -> 44.1k s16 Q15 (fused kernel, IO 2)
 planar  48k -> 44.1k fp32, planar tracks and mixes (fused kernel, PL)
 conv    48k -> 44.1k, s16 tracks into the fp32 mix (fused kernel, IO 1)
@@ -373,6 +374,34 @@ def _mono(a, name, ntr, B, fi, fo, N):
     report(name, f"{name}: {B} mixes x {ntr} mono f32 tracks x {N} frames, {fi}->{fo} f32 mix",
            B * ntr * N, B * ntr * N * 4 + B * F * 4, w, k, m, launches=launches,
            kernel="k_rs147_mix MONO" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
+           parity_check=parity(a, chk))
+
+
+def c1s16(a):
+    """Config 1's own form (mono s16 44.1k -> 48k, unity Q15 gain), batched:
+    8192 clips through Mixer(44100, 48000, 1, "s16"), the generic kernel."""
+    B, N = 16 * a.mixes, 441000
+    m = xm.Mixer(44100, 48000, 1, "s16", mem="device")
+    ramps = [dict(gain0_q15=32768)]
+    m.set_tracks(ramps)
+    F = m.out_frames(N)
+    x = torch.empty((B, N), dtype=torch.int16, device="cuda")
+    y = torch.empty((B, F), dtype=torch.int16, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "s16", SEED, 0, B, 1, N, 0, s.cuda_stream)
+    m.set_stream(s.cuda_stream)
+    w, k = timed(lambda: m.process_strided(x.data_ptr(), N, N, y.data_ptr(), F, B, N), a.steps, a.warmup, s)
+    fast, launches = m.timing().fast_launches, m.timing().n_launches
+
+    def chk():
+        for b in ends(B):
+            want = CO.resample_mix_s16([x[b].cpu().numpy()[:, None]], ramps, 160, 147)
+            if not beq(y[b].cpu().numpy()[:, None], want):
+                return False
+        return True
+    report("c1s16", f"c1s16: {B} mono s16 clips x {N} frames, 44100->48000 s16 (config 1's form)",
+           B * N, B * N * 2 + B * F * 2, w, k, m, launches=launches,
+           kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 
