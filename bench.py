@@ -41,9 +41,14 @@ Also reported (one JSON line on rank 0):
                  traffic: corrected PMC bytes per launch from the newest
                  profiles/*traffic*.json (an earlier rocprofv3 pass; the
                  file is named in traffic_source).
-  cpu_baseline — the C restatement (oracle/, "port") on a bounded sample of
-                 the same workload on this process's allotted host cores
-                 (sched_getaffinity), and on 1 core.
+  cpu_baseline — the library's own host CPU backend (n_devices = 0,
+                 xm-audio-utils_amd/src/cpu: the same C API call, bit-identical
+                 results) on a bounded sample of the same workload, in a child
+                 process on this process's allotted host cores
+                 (sched_getaffinity / OMP_NUM_THREADS) and in one on 1 core.
+                 The reference has no code, so this C path is
+                 the "reference CPU path" of BASELINE.json:5; oracle/ stays
+                 the checker.
   parity_check — after the timed loop every shard's first and last mix are
                  bit-compared with the oracle (true = all equal).
 """
@@ -107,7 +112,8 @@ def parse(argv=None):
     ap.add_argument("--mixes5", type=int, default=512, help="config 5: mixes (all devices)")
     ap.add_argument("--tracks5", type=int, default=64, help="config 5: tracks per mix (all devices)")
     ap.add_argument("--cpu-mixes", type=int, default=48, help="mixes in the CPU-baseline sample")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU-baseline sample")
+    ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)   # the baseline's child process
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fill", choices=["synth", "zero", "tiny"], default="synth",
                     help="dev only: input data (synth = the bench's synthetic PCM)")
@@ -192,51 +198,65 @@ def _timed_passes(fn, seconds, max_passes=200):
     return passes, dt, used
 
 
-def cpu_baseline(args, ramps):
-    """The oracle's C restatement (same arithmetic) on a bounded sample of the
+def _cpu_child(args, threads, mixes, seconds, config="headline"):
+    """One CPU-backend measurement in a child process (the pool's thread count
+    is fixed per process: XM_CPU_THREADS).  The child never touches a GPU."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-only", "--config", config, "--cpu-mixes", str(mixes),
+           "--cpu-seconds", str(seconds), "--tracks", str(args.tracks), "--frames", str(args.frames),
+           "--tracks5", str(args.tracks5)]
+    env = dict(os.environ, XM_CPU_THREADS=str(threads))
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode or not lines:
+        raise RuntimeError(f"cpu baseline child failed (rc {p.returncode}): {p.stderr[-600:]}")
+    return json.loads(lines[-1])
+
+
+def run_cpu_only(args):
+    """--cpu-only (child): whole passes of the library's CPU backend over a
+    sample of the workload, for about --cpu-seconds; prints one JSON line."""
+    import xmaudio as xm
+    if args.config == "c5":
+        B, ntr, N = args.cpu_mixes, args.tracks5, args.frames
+        x = np.empty((B, ntr, N, 2), np.int16)
+        xm.synth(x.ctypes.data, "s16", SEED, 1000, B * ntr, 2, N, device="cpu")
+        m = xm.Mixer(48000, 48000, 2, "s16", device="cpu")
+        m.set_tracks(RAMPS64[:ntr])
+    else:
+        B, ntr, N = args.cpu_mixes, args.tracks, args.frames
+        x = np.empty((B, ntr, N, 2), np.float32)
+        xm.synth(x.ctypes.data, "f32", SEED, 0, B * ntr, 2, N, device="cpu")
+        m = xm.Mixer(48000, 44100, 2, "f32", device="cpu")
+        m.set_tracks(RAMPS[:ntr] if ntr <= len(RAMPS) else (RAMPS * ((ntr + 7) // 8))[:ntr])
+    m.process(x)   # warm: pool threads, page faults of the output
+    passes, dt, _ = _timed_passes(lambda: m.process(x), args.cpu_seconds)
+    print(json.dumps({"samples": int(x.size) * passes, "seconds": dt, "passes": passes, "mixes": B,
+                      "threads": int(os.environ.get("XM_CPU_THREADS", "0"))}), flush=True)
+
+
+def cpu_baseline(args, ramps, config="headline"):
+    """The library's CPU backend (n_devices = 0) on a bounded sample of the
     workload: whole passes over --cpu-mixes mixes on every allotted core for
-    about --cpu-seconds, then on one core for about a quarter of that."""
-    import c_oracle as CO
-    nmix = args.cpu_mixes
-    x = np.empty((nmix, args.tracks, args.frames, 2), np.float32)
-    for b in range(nmix):
-        for t in range(args.tracks):
-            x[b, t] = CO.gen_f32(SEED, b * args.tracks + t, 2, args.frames)
+    about --cpu-seconds, then over 2 mixes on one core for half of that."""
     threads, host = allotted_cores()
-
-    def run(xs, nth, seconds):
-        passes, dt, used = _timed_passes(lambda: CO.batch_resample_mix_f32(xs, ramps, 147, 160, threads=nth)[1],
-                                         seconds)
-        return xs.size * passes, dt, passes, used
-
-    samples, dt, passes, used = run(x, threads, args.cpu_seconds)
-    x1 = x[:2]
-    s1, dt1, p1, _ = run(x1, 1, args.cpu_seconds / 4)
-    del x
-    return {"value": round(samples / dt / 1e6, 2), "unit": "Msamples/s", "cores": int(used), "kind": "port",
-            "value_1core": round(s1 / dt1 / 1e6, 2), "cpu_model": cpu_model(), "host_cpus": host,
-            "cores_note": f"{used} threads = this process's allotted share (sched_getaffinity / OMP_NUM_THREADS) "
+    mixes = args.cpu_mixes if config == "headline" else max(1, args.cpu_mixes // 12)   # c5: 64-track mixes
+    a = _cpu_child(args, threads, mixes, args.cpu_seconds, config)
+    one = _cpu_child(args, 1, 2, args.cpu_seconds / 2, config)
+    ntr = args.tracks5 if config == "c5" else args.tracks
+    what = (f"{ntr} s16 tracks (Q15 mix)" if config == "c5"
+            else f"{ntr} tracks x {args.frames} frames x 2 ch fp32, 48k->44.1k + ramped mix")
+    return {"value": round(a["samples"] / a["seconds"] / 1e6, 2), "unit": "Msamples/s", "cores": int(threads),
+            "kind": "port", "value_1core": round(one["samples"] / one["seconds"] / 1e6, 2),
+            "path": "libxm_audio's host CPU backend (XmMixerConfig.n_devices = 0; xm-audio-utils_amd/src/cpu, "
+                    "-O3 -ffp-contract=off, AVX-512/AVX2 vector tap loops, pthread pool); results bit-identical "
+                    "to the GPU's. The reference has no code, so this is the build's own CPU path (SURVEY.md §0)",
+            "cpu_model": cpu_model(), "host_cpus": host,
+            "cores_note": f"{threads} threads = this process's allotted share (sched_getaffinity / OMP_NUM_THREADS) "
                           f"of the host's {host} CPUs",
-            "sample": f"{passes} passes over {nmix} mixes x {args.tracks} tracks x {args.frames} frames x 2 ch fp32 "
-                      f"({samples / 1e6:.0f} M input samples, {dt:.2f} s wall, {used} threads); 1 core: {p1} passes "
-                      f"over 2 mixes ({s1 / 1e6:.0f} M samples, {dt1:.2f} s); oracle/xm_oracle.c -O3 "
-                      f"-ffp-contract=off, OpenMP over mixes"}
-
-
-def cpu_baseline_c5(args, ramps, ntr, N):
-    """config 5's CPU baseline: the oracle's Q15 mix (xo_batch_mix_s16) over a
-    bounded sample of 64-track mixes on the allotted cores, then on one core."""
-    import c_oracle as CO
-    nmix = 4
-    x = np.stack([np.stack([CO.gen_s16(SEED, 1000 + b * ntr + t, 2, N) for t in range(ntr)]) for b in range(nmix)])
-    threads, host = allotted_cores()
-    p, dt, used = _timed_passes(lambda: CO.batch_mix_s16(x, ramps, threads=threads)[1], args.cpu_seconds / 2)
-    p1, dt1, _ = _timed_passes(lambda: CO.batch_mix_s16(x[:1], ramps, threads=1)[1], args.cpu_seconds / 4)
-    return {"value": round(x.size * p / dt / 1e6, 2), "unit": "Msamples/s", "cores": int(used), "kind": "port",
-            "value_1core": round(x[:1].size * p1 / dt1 / 1e6, 2), "cpu_model": cpu_model(), "host_cpus": host,
-            "sample": f"{p} passes over {nmix} mixes x {ntr} s16 tracks x {N} frames x 2 ch ({dt:.2f} s, "
-                      f"{used} threads); 1 core: {p1} passes over 1 mix ({dt1:.2f} s); oracle/xm_oracle.c "
-                      f"xo_batch_mix_s16, OpenMP over mixes"}
+            "sample": f"{a['passes']} passes over {a['mixes']} mixes x {what} ({a['samples'] / 1e6:.0f} M input "
+                      f"samples, {a['seconds']:.2f} s, {threads} threads); 1 core: {one['passes']} passes over "
+                      f"{one['mixes']} mixes ({one['samples'] / 1e6:.0f} M samples, {one['seconds']:.2f} s)"}
 
 
 def parity_check(x, y, idx, ramps):
@@ -430,7 +450,7 @@ def c5_line(args, *, n_gpus, shards, B, ntr, N, value, ms_per_step, ok, mode, pa
                      "alg_bytes_per_device_step": dev_bytes, "xgmi_bytes_per_device_step": xgmi,
                      "note": "per-device algorithmic HBM bytes over the whole step's wall time "
                              "(partial kernel + exchange + finish)"},
-        "cpu_baseline": None if args.no_cpu else cpu_baseline_c5(args, RAMPS64[:ntr], ntr, N),
+        "cpu_baseline": None if args.no_cpu else cpu_baseline(args, RAMPS64[:ntr], config="c5"),
     }
     if ok is not None:
         line["parity_check"] = ok
@@ -553,6 +573,9 @@ def run_c5_ranked(args):
 
 def main(argv=None):
     args = parse(argv)
+    if args.cpu_only:
+        run_cpu_only(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     mode, devs = plan(args, world, torch.cuda.device_count())
     if args.config == "c5":

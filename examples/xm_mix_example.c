@@ -41,6 +41,7 @@ int main(void)
     cfg.sample_fmt = XM_FMT_F32;
     cfg.mem_kind = XM_MEM_HOST;
     cfg.device = 0;
+    cfg.n_devices = 1;   /* one GPU (0 would select the host CPU backend) */
     int st = 0;
     XmAudioMixer *mx = xm_audio_mixer_create_ex(&cfg, &st);
     if (!mx) return fail("xm_audio_mixer_create_ex", st);

@@ -59,6 +59,7 @@ int main(void)
     cfg.channels = 2;
     cfg.sample_fmt = XM_FMT_F32;
     cfg.mem_kind = XM_MEM_HOST;
+    cfg.n_devices = 1;   /* one GPU (0 would select the host CPU backend) */
     int st = 0;
     XmAudioMixer *one = xm_audio_mixer_create_ex(&cfg, &st);
     if (!one) return fail("xm_audio_mixer_create_ex", st);

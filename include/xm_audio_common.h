@@ -87,13 +87,26 @@ typedef struct XmGainRamp {
     int32_t reserved;
 } XmGainRamp;
 
+/* Device ordinal of the host CPU backend (SURVEY.md §8(b) "n_devices (0 =
+ * CPU)"): the library's own C implementation of every job, in the same
+ * arithmetic as the gfx950 kernels (bit-identical results), run on the host
+ * cores of the calling process (XM_CPU_THREADS threads if set, else one per
+ * CPU of its affinity mask).  A mixer is created on it by
+ * XmMixerConfig.n_devices == 0, an effects chain by XmEffectsConfig.device ==
+ * XM_DEVICE_CPU or xm_effects_create(rate, channels, 0), synthetic PCM by
+ * xm_synth_pcm(..., XM_DEVICE_CPU, NULL).  Its memory is host memory: both
+ * XmMemKind values mean host pointers, used in place.  Chosen at create time
+ * only: a GPU handle never falls back to it. */
+#define XM_DEVICE_CPU (-1)
+
 /* Human-readable text for a status code (static storage). */
 XM_API const char *xm_strerror(int status);
 
 /* Library version string, e.g. "xm-audio-mi355x 0.1.0 (gfx950)". */
 XM_API const char *xm_version(void);
 
-/* Number of HIP devices visible to this process (0 if none / runtime absent). */
+/* Number of HIP devices visible to this process (0 if none / runtime absent;
+ * the CPU backend is not counted). */
 XM_API int xm_device_count(void);
 
 /* ---- rational resampler design (exported for tests and tools) ----------
@@ -120,7 +133,8 @@ XM_API size_t xm_resample_out_frames(int in_rate, int out_rate, size_t frames_in
  * z = splitmix64_mix(seed + idx * 0x9E3779B97F4A7C15),
  * F32: ((int)(z >> 40) - 2^23) * 2^-23  (uniform in [-1, 1), exact)
  * S16: (int16)(z >> 48).
- * dst must be device memory of `device`; stream may be NULL (synchronous). */
+ * dst must be device memory of `device` (host memory for XM_DEVICE_CPU);
+ * stream may be NULL (synchronous). */
 XM_API int xm_synth_pcm(void *dst, int sample_fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,
                  int channels, int64_t frames, int device, void *hip_stream);
 

@@ -73,9 +73,10 @@ typedef struct XmMixerConfig {
     int32_t channels;     /* 1 or 2 */
     int32_t sample_fmt;   /* XmSampleFmt, input and output */
     int32_t mem_kind;     /* XmMemKind of the in/out pointers */
-    int32_t device;       /* HIP device ordinal the handle runs on */
+    int32_t device;       /* HIP device ordinal the handle runs on (ignored when n_devices == 0) */
     int32_t flags;        /* 0 or XM_MIXER_OUT_CONVERT | XM_MIXER_IN_CONVERT | XM_MIXER_PLANAR */
-    int32_t n_devices;    /* 0 or 1: one device; n > 1: devices device .. device+n-1 */
+    int32_t n_devices;    /* 0: the host CPU backend (XM_DEVICE_CPU);
+                             1: one GPU, `device`; n > 1: GPUs device .. device+n-1 */
 } XmMixerConfig;
 
 typedef struct XmTrackDesc {
@@ -98,8 +99,13 @@ typedef struct XmMixerTiming {
 } XmMixerTiming;
 
 /* Create a mixer.  Returns NULL on failure; *status (if non-NULL) gets the
- * reason.  Fails with XM_EDEVICE when no GPU / HIP runtime is usable: there
- * is no CPU fallback in the product library. */
+ * reason.  n_devices == 0 creates it on the host CPU backend (XM_DEVICE_CPU:
+ * every call runs on the host cores, in place on host pointers, with the
+ * GPU's results bit for bit; no GPU needed).  n_devices >= 1 creates it on
+ * GPUs and fails with XM_EDEVICE when they are not usable: a GPU handle never
+ * falls back to the CPU.  On a CPU handle set_stream is accepted and
+ * ignored (calls are synchronous), mix_spanning_s16 runs as one device, and
+ * the timing reports host wall time in kernel_ms. */
 XM_API XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status);
 XM_API XmAudioMixer *xm_audio_mixer_create(const XmMixerConfig *cfg);
 

@@ -258,6 +258,46 @@ def main():
         sp.mix_spanning_s16([a.ctypes.data for a in ins], 480, per * 480, [o.ctypes.data for o in outs], 480, 4, 240)
         check(f"mix_spanning_s16 {devs}", beq(np.concatenate(outs), want64))
 
+    # the CPU backend (n_devices = 0 / XM_DEVICE_CPU) under the sanitizers:
+    # the resampler's staged blocks, windows, pointer tables, effects and
+    # their streams, timelines, partials
+    x = f32_tracks(3, 8, 1601, base=900)
+    for mem in ("host", "device"):
+        c = xm.Mixer(48000, 44100, 2, "f32", mem=mem, device="cpu")
+        c.set_tracks(RAMPS)
+        check(f"cpu backend: f32 48k->44.1k 8-track mix ({mem})",
+              beq(c.process(x), CO.batch_resample_mix_f32(x, RAMPS, 147, 160, threads=1)[0]))
+    c = xm.Mixer(44100, 48000, 1, "s16", device="cpu")
+    xs = O.gen_s16(SEED, 0, 1, 3001)
+    check("cpu backend: config-1 form (mono s16 44.1k->48k)", beq(c.process(xs[None, None])[0], CO.resample_s16(xs, 160, 147)))
+    c = xm.Mixer(48000, 44100, 2, "f32", device="cpu")
+    c.set_tracks(RAMPS[:3])
+    c.stream_begin(2)
+    xt = f32_tracks(2, 3, 2000, base=950)
+    parts = [c.stream_push(xt[:, :, a:b]) for a, b in ((0, 1), (1, 700), (700, 701), (701, 2000))] + [c.stream_flush()]
+    check("cpu backend: streamed mix == whole", beq(np.concatenate(parts, axis=1),
+                                                    CO.batch_resample_mix_f32(xt, RAMPS[:3], 147, 160)[0]))
+    ce = xm.Effects(44100, 2, device="cpu")
+    for sq in sos:
+        ce.add_biquad(sq)
+    ce.add_fir(h)
+    xe = f32_tracks(3, 1, 3000, base=980)[:, 0]
+    want = [CO.fir_f32(CO.biquad_f32(v, sos), h) for v in xe]
+    check("cpu backend: effects chain", all(beq(a, b) for a, b in zip(ce.process(xe), want)))
+    ce.stream_reset(3)
+    got = np.concatenate([ce.process_stream(np.ascontiguousarray(xe[:, a:b])) for a, b in ((0, 5), (5, 1000), (1000, 3000))],
+                         axis=1)
+    check("cpu backend: effects stream == whole", all(beq(a, b) for a, b in zip(got, want)))
+    cm = xm.Mixer(48000, 44100, 2, "f32", device="cpu")
+    cm.set_tracks(RAMPS[:2])
+    ce2 = xm.Effects(44100, 2, device="cpu")
+    for sq in sos:
+        ce2.add_biquad(sq)
+    cm.set_track_effects(ce2)
+    xk = f32_tracks(2, 2, 1500, base=990)
+    wk = [CO.mix_f32([CO.biquad_f32(CO.resample_f32(t, 147, 160), sos) for t in xk[b]], RAMPS[:2]) for b in range(2)]
+    check("cpu backend: per-track effects (config 4 form)", beq(cm.process(xk), np.stack(wk)))
+
     # argument errors never reach a kernel
     bad = 0
     for fn in (lambda: xm.Mixer(0, 48000), lambda: xm.Mixer(48000, 44100, 3),

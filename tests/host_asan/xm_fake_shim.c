@@ -7,7 +7,9 @@
  * (SURVEY.md §4 "fake-device backend", §5 "Sanitizers").
  *
  * It is linked only into tests/host_asan/libxm_audio_asan.so (Makefile next
- * to this file), never into the product library, which has no CPU path.
+ * to this file), never into the product library.
+ * It stands in for the GPU backend table (xmh_gpu, csrc/xm_shim.h); the
+ * product's CPU backend (src/cpu/) is linked in unchanged beside it.
  * "Device memory" is host memory; launches run the kernels' contract
  * (include/xm_audio_common.h) in plain C with the same operation order, so
  * tests/test_host_asan.py can also compare its outputs with the oracle.  Every
@@ -30,52 +32,52 @@ static int fake_devices(void)
     return e ? atoi(e) : 1;
 }
 
-/* failure injection for the checks: xmh_set_device(dev) fails while dev == fail_dev */
+/* failure injection for the checks: fk_set_device(dev) fails while dev == fail_dev */
 static int fail_dev = -1;
 __attribute__((visibility("default"))) void xm_fake_fail_device(int dev) { fail_dev = dev; }
 
-int xmh_device_count(void) { return fake_devices(); }
-int xmh_set_device(int dev) { return dev >= 0 && dev < fake_devices() && dev != fail_dev ? 0 : -1001; }
+static int fk_device_count(void) { return fake_devices(); }
+static int fk_set_device(int dev) { return dev >= 0 && dev < fake_devices() && dev != fail_dev ? 0 : -1001; }
 
-int xmh_malloc(void **p, size_t bytes)
+static int fk_malloc(void **p, size_t bytes)
 {
     *p = malloc(bytes ? bytes : 16);
     return *p ? 0 : XM_ENOMEM_;
 }
 
-void xmh_free(void *p) { free(p); }
-int xmh_host_alloc(void **p, size_t bytes) { return xmh_malloc(p, bytes); }
-void xmh_host_free(void *p) { free(p); }
+static void fk_free(void *p) { free(p); }
+static int fk_host_alloc(void **p, size_t bytes) { return fk_malloc(p, bytes); }
+static void fk_host_free(void *p) { free(p); }
 
 static int fake_stream_obj;
-int xmh_stream_create(void **s)
+static int fk_stream_create(void **s)
 {
     *s = &fake_stream_obj;
     return 0;
 }
-void xmh_stream_destroy(void *s) { (void)s; }
-int xmh_stream_sync(void *s)
+static void fk_stream_destroy(void *s) { (void)s; }
+static int fk_stream_sync(void *s)
 {
     (void)s;
     return 0;
 }
 
-int xmh_memcpy_h2d(void *dst, const void *src, size_t n, void *s)
+static int fk_memcpy_h2d(void *dst, const void *src, size_t n, void *s)
 {
     (void)s;
     if (n) memmove(dst, src, n);
     return 0;
 }
-int xmh_memcpy_d2h(void *dst, const void *src, size_t n, void *s) { return xmh_memcpy_h2d(dst, src, n, s); }
-int xmh_memcpy_d2d(void *dst, const void *src, size_t n, void *s) { return xmh_memcpy_h2d(dst, src, n, s); }
-int xmh_memcpy_peer(void *dst, int dd, const void *src, int sd, size_t n, void *s)
+static int fk_memcpy_d2h(void *dst, const void *src, size_t n, void *s) { return fk_memcpy_h2d(dst, src, n, s); }
+static int fk_memcpy_d2d(void *dst, const void *src, size_t n, void *s) { return fk_memcpy_h2d(dst, src, n, s); }
+static int fk_memcpy_peer(void *dst, int dd, const void *src, int sd, size_t n, void *s)
 {
     (void)dd;
     (void)sd;
-    return xmh_memcpy_h2d(dst, src, n, s);
+    return fk_memcpy_h2d(dst, src, n, s);
 }
 
-int xmh_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height, void *s)
+static int fk_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height, void *s)
 {
     (void)s;
     if (!width || !height) return 0;
@@ -84,7 +86,7 @@ int xmh_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_
     return 0;
 }
 
-int xmh_memset(void *dst, int v, size_t n, void *s)
+static int fk_memset(void *dst, int v, size_t n, void *s)
 {
     (void)s;
     if (n) memset(dst, v, n);
@@ -92,19 +94,19 @@ int xmh_memset(void *dst, int v, size_t n, void *s)
 }
 
 static int fake_event_obj;
-int xmh_event_create(void **e)
+static int fk_event_create(void **e)
 {
     *e = &fake_event_obj;
     return 0;
 }
-void xmh_event_destroy(void *e) { (void)e; }
-int xmh_event_record(void *e, void *s)
+static void fk_event_destroy(void *e) { (void)e; }
+static int fk_event_record(void *e, void *s)
 {
     (void)e;
     (void)s;
     return 0;
 }
-int xmh_event_elapsed(float *ms, void *e0, void *e1)
+static int fk_event_elapsed(float *ms, void *e0, void *e1)
 {
     (void)e0;
     (void)e1;
@@ -112,13 +114,13 @@ int xmh_event_elapsed(float *ms, void *e0, void *e1)
     return 0;
 }
 
-int xmh_pointer_is_device(const void *p)
+static int fk_pointer_is_device(const void *p)
 {
     (void)p;
     return 0;
 }
 
-const char *xmh_arch_name(void) { return "fake-cpu"; }
+static const char *fk_arch_name(void) { return "fake-cpu"; }
 
 /* ---- the kernels' arithmetic contract in C (include/xm_audio_common.h) ---- */
 static float gain_f32(const XmhGain *g, int64_t n)
@@ -179,7 +181,7 @@ static void store(const XmhMixJob *j, int64_t b, int64_t i, int s16, int32_t acc
     else ((float *)out_ptr(j, b, 4))[i] = accf + 0.0f;
 }
 
-int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
+static int fk_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
 {
     (void)stream;
     (void)n_fast;
@@ -224,13 +226,13 @@ int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fas
 
 /* the fused kernel's streaming windows: not modelled here, the host falls
  * back to the generic window job */
-int xmh_launch_mix_window(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
+static int fk_launch_mix_window(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
 {
     (void)j; (void)stream; (void)n_launches; (void)n_fast;
     return -1003;
 }
 
-int xmh_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
+static int fk_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
 {
     (void)stream;
     const int C = j->channels, s16 = j->fmt == 1;
@@ -254,7 +256,7 @@ int xmh_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
     return 0;
 }
 
-int xmh_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
+static int fk_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
                           int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream)
 {
     (void)stream;
@@ -269,7 +271,7 @@ int xmh_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride
 
 /* biquad: sosfilt order, state [clip][section][z0,z1][ch] when streaming;
  * FIR: upfirdn order, the K-1 frames before the block from hist_in */
-int xmh_launch_fx(const XmhFxJob *j, void *stream, int *n_launches)
+static int fk_launch_fx(const XmhFxJob *j, void *stream, int *n_launches)
 {
     (void)stream;
     const int C = j->channels;
@@ -332,7 +334,7 @@ int xmh_launch_fx(const XmhFxJob *j, void *stream, int *n_launches)
     return 0;
 }
 
-int xmh_fast_table_check(const float *H, int L, int M, int T)
+static int fk_fast_table_check(const float *H, int L, int M, int T)
 {
     (void)H;
     (void)L;
@@ -348,7 +350,7 @@ static uint64_t mix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
-int xmh_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips, int channels, int64_t frames,
+static int fk_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips, int channels, int64_t frames,
               void *stream)
 {
     (void)stream;
@@ -376,7 +378,7 @@ static int fake_comm_slot[64];
 static FakeRs fake_pending[64];
 static int fake_npend, fake_in_group;
 
-int xmh_comm_init_all(void **comms, int n, const int *devs)
+static int fk_comm_init_all(void **comms, int n, const int *devs)
 {
     (void)devs;
     if (n < 1 || n > 64) return -1002;
@@ -388,7 +390,7 @@ int xmh_comm_init_all(void **comms, int n, const int *devs)
     return 0;
 }
 
-void xmh_comm_destroy(void *comm) { (void)comm; }
+static void fk_comm_destroy(void *comm) { (void)comm; }
 
 static void fake_flush(void)
 {
@@ -403,13 +405,13 @@ static void fake_flush(void)
     fake_npend = 0;
 }
 
-int xmh_group_start(void)
+static int fk_group_start(void)
 {
     fake_in_group = 1;
     return 0;
 }
 
-int xmh_group_end(void)
+static int fk_group_end(void)
 {
     fake_in_group = 0;
     if (fake_npend != fake_comm_n) return -1002;
@@ -417,7 +419,7 @@ int xmh_group_end(void)
     return 0;
 }
 
-int xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s)
+static int fk_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s)
 {
     (void)s;
     if (!fake_in_group || fake_npend >= 64) return -1002;
@@ -425,4 +427,14 @@ int xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count
     return 0;
 }
 
-int xmh_comm_check(void *comm) { return comm ? 0 : -1002; }
+static int fk_comm_check(void *comm) { return comm ? 0 : -1002; }
+
+const XmhBackend xmh_gpu = {
+    "fake-gfx950",
+    fk_device_count, fk_set_device, fk_malloc, fk_free, fk_host_alloc, fk_host_free,
+    fk_stream_create, fk_stream_destroy, fk_stream_sync, fk_memcpy_h2d, fk_memcpy_d2h, fk_memcpy_d2d,
+    fk_memset, fk_memcpy2d, fk_event_create, fk_event_destroy, fk_event_record, fk_event_elapsed,
+    fk_pointer_is_device, fk_memcpy_peer, fk_comm_init_all, fk_comm_destroy, fk_group_start, fk_group_end,
+    fk_reduce_scatter_i32, fk_comm_check, fk_arch_name, fk_launch_mix, fk_launch_mix_window, fk_launch_fx,
+    fk_launch_mix_placed, fk_launch_finish_s16, fk_fast_table_check, fk_synth,
+};

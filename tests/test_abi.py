@@ -64,8 +64,10 @@ def test_out_frames(xm):
     assert xm.out_frames(48000, 44100, 161) == -(-161 * 147 // 160)
 
 
-def test_no_cpu_fallback_without_gpu(xm):
-    """The product has no CPU path: with no GPU, create must fail loudly."""
+def test_gpu_handle_without_gpu_fails(xm):
+    """GPU handles (the default n_devices = 1) never fall back to the CPU
+    backend: with no GPU, create fails loudly.  The CPU backend is chosen
+    only by n_devices = 0 / XM_DEVICE_CPU (tests/test_cpu_backend.py)."""
     if xm.device_count() > 0:
         pytest.skip("GPU present")
     with pytest.raises(xm.XmError) as e:

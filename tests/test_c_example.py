@@ -1,7 +1,9 @@
 """The drop-in boundary from C: examples/xm_mix_example.c compiles against
 include/*.h with plain gcc, links libxm_audio.so, and runs.  On a host without
-a GPU the library must refuse loudly (XM_EDEVICE, exit 2) instead of falling
-back to CPU; on the GPU box the example must complete (exit 0)."""
+a GPU the GPU examples must refuse loudly (XM_EDEVICE, exit 2) instead of
+falling back to the CPU; on the GPU box they must complete (exit 0).  The
+config-1 example asks for the CPU backend (n_devices = 0) and runs anywhere."""
+import hashlib
 import os
 import subprocess
 
@@ -81,3 +83,15 @@ def test_multi_example_runs_on_gpu(tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     assert "bit-identical to one device" in p.stdout
     assert "config 5:" in p.stdout
+
+
+def test_config1_cpu_example(tmp_path):
+    """BASELINE.json:7 from plain C with no GPU: n_devices = 0 reproduces the
+    committed config-1 digest (scipy-pinned)."""
+    from conftest import manifest
+    exe = _build(tmp_path, "xm_config1_cpu")
+    out = tmp_path / "y.raw"
+    p = subprocess.run([str(exe), str(out)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "441000 -> 480000 frames" in p.stdout
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == manifest()["config1_sha256"]

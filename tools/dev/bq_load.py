@@ -23,7 +23,7 @@ for it in range(2):
 # [workgroup][chain, producer, load, store][work, barrier wait])
 import ctypes
 import numpy as np
-fn = getattr(xm._lib, "xmh_dev_bq_prof", None)
+fn = getattr(xm._lib, "xm_dev_bq_prof", None)
 if fn is not None:
     buf = np.zeros(4096, np.uint64)
     fn(buf.ctypes.data_as(ctypes.c_void_p))
@@ -33,7 +33,7 @@ if fn is not None:
     for k, name in enumerate(("chain", "producer", "load", "store")):
         print("%-8s wave, cycles per 64-frame step: work %.0f  barrier/wait %.0f" % ((name,) + tuple(w[:, k].mean(0) / steps)),
               flush=True)
-fh = getattr(xm._lib, "xmh_dev_bq_hw", None)
+fh = getattr(xm._lib, "xm_dev_bq_hw", None)
 if fh is not None:
     hw = np.zeros(2048, np.uint32)
     fh(hw.ctypes.data_as(ctypes.c_void_p))

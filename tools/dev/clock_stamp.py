@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Dev only: the fused kernel's in-kernel clock (MI355X_MICROARCH.md "DVFS
+give-back" item 6) on the headline shape.
+
+Run against the diagnostic build, which stamps s_memtime / s_memrealtime once
+per wave around its whole run (csrc/xm_resample_fast.hip, XM_CLOCK_STAMPS):
+
+    make -C xm-audio-utils_amd ab AB=-DXM_CLOCK_STAMPS ABOUT=lib_clk FAST_PARTS=0
+    XM_AUDIO_LIB=$PWD/xm-audio-utils_amd/lib_clk/libxm_audio.so python tools/dev/clock_stamp.py
+
+It runs >= --seconds of back-to-back launches (random synthetic PCM), clears
+the stamps, runs --steps more and prints one JSON line: the aggregate clock
+(sum of shader cycles / sum of 100-MHz ticks), the mean wave lifetime and
+the wall time per launch of that build.  The stamped build's wall time is not
+the product's (its stamps add waits); read the clock, not the length.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "xm-audio-utils_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import xmaudio as xm  # noqa: E402
+from bench import RAMPS, SEED  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mixes", type=int, default=512)
+    ap.add_argument("--frames", type=int, default=480000)
+    ap.add_argument("--seconds", type=float, default=2.5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--fill", choices=["synth", "zero"], default="synth")
+    ap.add_argument("--label", default="")
+    args = ap.parse_args()
+    fn = getattr(xm._lib, "xm_dev_clock", None)
+    if fn is None:
+        raise SystemExit("clock_stamp.py: the loaded library has no xm_dev_clock (build with -DXM_CLOCK_STAMPS)")
+    fn.restype, fn.argtypes = C.c_int, [C.POINTER(C.c_ulonglong)]
+    B, ntr, N = args.mixes, 8, args.frames
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device", device=0)
+    m.set_tracks(RAMPS)
+    F = m.out_frames(N)
+    x = torch.empty((B, ntr, N, 2), dtype=torch.float32, device="cuda")
+    y = torch.empty((B, F, 2), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B * ntr, 2, N, 0, s.cuda_stream)
+    if args.fill == "zero":
+        x.zero_()
+    m.set_stream(s.cuda_stream)
+    torch.cuda.synchronize()
+
+    def step():
+        m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)
+
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.seconds:   # warm the clock: back-to-back launches
+        for _ in range(20):
+            step()
+        torch.cuda.synchronize()
+    buf = (C.c_ulonglong * 4)()
+    fn(buf)   # clear
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.steps
+    fn(buf)
+    cyc, ticks, waves = buf[0], buf[1], buf[2]
+    print(json.dumps({"label": args.label, "lib": os.environ.get("XM_AUDIO_LIB", ""), "mixes": B, "frames": N,
+                      "fill": args.fill, "steps": args.steps, "waves": waves,
+                      "clock_ghz": round(cyc / ticks * 0.1, 4) if ticks else None,
+                      "wave_us_mean": round(ticks / waves * 0.01, 2) if waves else None,
+                      "wave_cycles_mean": round(cyc / waves) if waves else None,
+                      "wall_ms_per_launch_stamped_build": round(wall * 1e3, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -5,7 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include "xm_shim.h"
+#include "xm_gpu.h"
 
 #define XM_DEV __device__ __forceinline__
 

@@ -1295,7 +1295,7 @@ __global__ __launch_bounds__(256) void k_synth(void *out, int fmt, uint64_t seed
 
 }  // namespace
 
-extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
+extern "C" int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream)
 {
     if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
     if (j->n_clips == 0 || j->frames == 0) return 0;
@@ -1318,7 +1318,7 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
         auto pk = j->channels == 2 ? (j->state ? k_biquad_pc<2, true> : k_biquad_pc<2, false>)
                                    : (j->state ? k_biquad_pc<1, true> : k_biquad_pc<1, false>);
         const int kpw = std::min(16 / j->n_sos * (4 / j->channels), PC_KPW);
-        if (xmh_func_lds((const void *)pk, (int)PC_LDS)) return -1001;   // once per (kernel, device)
+        if (xmg_func_lds((const void *)pk, (int)PC_LDS)) return -1001;   // once per (kernel, device)
         XmhFxJob jj = *j;
         hipLaunchKernelGGL(pk, dim3((unsigned)((j->n_clips + kpw - 1) / kpw)), dim3(256), PC_LDS,
                            (hipStream_t)stream, jj);
@@ -1331,24 +1331,24 @@ extern "C" int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream)
                                        : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>));
     const int kpw = mf ? std::min(16 / j->n_sos * (4 / j->channels), BQ_KPW) : std::min(64 / j->n_sos, BQ_KPW);
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
-    if (xmh_func_lds((const void *)kern, (int)BQ_LDS)) return -1001;   // once per (kernel, device)
+    if (xmg_func_lds((const void *)kern, (int)BQ_LDS)) return -1001;   // once per (kernel, device)
     XmhFxJob jj = *j;
     hipLaunchKernelGGL(kern, grid, dim3(128), BQ_LDS, (hipStream_t)stream, jj);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
 
 #ifdef XM_BQ_PROF
-extern "C" __attribute__((visibility("default"))) int xmh_dev_bq_prof(uint64_t *host)
+extern "C" __attribute__((visibility("default"))) int xm_dev_bq_prof(uint64_t *host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_prof), sizeof(g_bq_prof)) == hipSuccess ? 0 : -1;
 }
-extern "C" __attribute__((visibility("default"))) int xmh_dev_bq_hw(uint32_t *host)
+extern "C" __attribute__((visibility("default"))) int xm_dev_bq_hw(uint32_t *host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_hw), sizeof(g_bq_hw)) == hipSuccess ? 0 : -1;
 }
 #endif
 
-extern "C" int xmh_launch_fx_fir(const XmhFxJob *j, void *stream)
+extern "C" int xmg_launch_fx_fir(const XmhFxJob *j, void *stream)
 {
     const int K = j->fir_len;
     const size_t lds = (size_t)(((K + 3) & ~3) + (FIR_CHUNK + K) * j->channels) * sizeof(float);
@@ -1368,19 +1368,19 @@ extern "C" int xmh_launch_fx_fir(const XmhFxJob *j, void *stream)
         const size_t lds_rb = std::max(rl, (size_t)FR_TILE * j->channels * sizeof(float));
         if (lds_rb > 160 * 1024) return -1003;
         auto kr = j->channels == 1 ? k_fir_rb<1> : k_fir_rb<2>;
-        if (lds_rb > 64 * 1024 && xmh_func_lds((const void *)kr, (int)lds_rb)) return -1001;
+        if (lds_rb > 64 * 1024 && xmg_func_lds((const void *)kr, (int)lds_rb)) return -1001;
         hipLaunchKernelGGL(kr, dim3((unsigned)((j->frames + FR_TILE - 1) / FR_TILE), (unsigned)j->n_clips),
                            64 * FR_WAVES, lds_rb, (hipStream_t)stream, *j);
         return hipGetLastError() == hipSuccess ? 0 : -1001;
     }
 #endif
     auto kern = j->channels == 1 ? k_fir<1> : k_fir<2>;
-    if (lds > 64 * 1024 && xmh_func_lds((const void *)kern, (int)lds)) return -1001;
+    if (lds > 64 * 1024 && xmg_func_lds((const void *)kern, (int)lds)) return -1001;
     hipLaunchKernelGGL(kern, grid, FIR_THREADS, lds, (hipStream_t)stream, *j);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
 
-extern "C" int xmh_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,
+extern "C" int xmg_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,
                          int channels, int64_t frames, void *stream)
 {
     const int64_t per_clip = frames * channels;

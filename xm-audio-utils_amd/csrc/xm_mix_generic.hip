@@ -436,7 +436,7 @@ template <typename K>
 int launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const XmhMixJob &j)
 {
     if (grid.x == 0 || grid.y == 0) return 0;
-    if (lds > 64 * 1024 && xmh_func_lds((const void *)kern, (int)lds)) return -1001;   // once per (kernel, device)
+    if (lds > 64 * 1024 && xmg_func_lds((const void *)kern, (int)lds)) return -1001;   // once per (kernel, device)
     hipLaunchKernelGGL(kern, grid, block, lds, s, j);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess && getenv("XM_DEBUG")) fprintf(stderr, "generic launch: %s\n", hipGetErrorString(e));
@@ -445,9 +445,9 @@ int launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s, const XmhMi
 
 }  // namespace
 
-// Generic launcher (called by xmh_launch_mix in xm_shim.hip when the fast
+// Generic launcher (called by xmg_launch_mix in xm_shim.hip when the fast
 // kernel does not apply).
-extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_launches)
+extern "C" int xmg_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_launches)
 {
     hipStream_t s = (hipStream_t)stream;
     const int C = j->channels;
@@ -496,7 +496,7 @@ extern "C" int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
     return rc;
 }
 
-extern "C" int xmh_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
+extern "C" int xmg_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches)
 {
     if (j->frames_out == 0 || j->n_mix == 0) return 0;
     if (!j->place || !j->in_ptrs || (j->channels != 1 && j->channels != 2)) return -22;
@@ -512,7 +512,7 @@ extern "C" int xmh_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_la
     return rc;
 }
 
-extern "C" int xmh_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
+extern "C" int xmg_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
                                      int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream)
 {
     if (batch <= 0 || samples <= 0) return 0;

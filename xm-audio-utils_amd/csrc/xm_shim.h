@@ -1,7 +1,18 @@
 /*
- * xm_shim.h — internal C ABI between the C host layer (src/ C files) and the HIP
- * side (csrc/ .hip files).  Plain C types only; every hipError_t is mapped to an
- * XM_* status inside the shim (SURVEY.md §8(b) "Shim exports").
+ * xm_shim.h — internal C ABI between the C host layer (src/ C files) and the
+ * compute backends.  Plain C types only; every hipError_t is mapped to an XM_*
+ * status inside the shim (SURVEY.md §8(b) "Shim exports").
+ *
+ * Two backends implement it ("The CPU backend exports the
+ * identical xmh_* set ... the backend is selected at create-time"):
+ *   xmh_gpu  csrc/xm_shim.hip and the gfx950 kernels (HIP device ordinals >= 0);
+ *   xmh_cpu  src/cpu/ — the library's own C implementation of the same jobs on
+ *            the host cores (SURVEY.md §1 layer L0-cpu), selected by the device
+ *            ordinal XMH_DEV_CPU (XmMixerConfig.n_devices == 0).
+ * The xmh_* functions below dispatch to the backend of the calling thread's
+ * current device, set by xmh_set_device() (src/xm_backend.c), the way HIP's
+ * own current device is per thread; every API call sets its handle's device
+ * first.  A thread that never called xmh_set_device() is on the GPU backend.
  *
  * Nothing here is public: callers use include/xm_audio_mixer.h and
  * include/xm_effects.h.
@@ -151,11 +162,6 @@ int  xmh_group_end(void);
 int  xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s);
 int  xmh_comm_check(void *comm);               /* XM_ECOMM on an asynchronous error */
 const char *xmh_arch_name(void);
-/* CUs of the current device (cached per device) */
-int  xmh_cu_count(void);
-/* hipFuncAttributeMaxDynamicSharedMemorySize >= bytes for kern on the current
- * device, set once per (kernel, device) */
-int  xmh_func_lds(const void *kern, int bytes);
 
 /* ---------- kernels ----------------------------------------------------------- */
 /* resample (if rs.L != rs.M) + gain + ordered track sum; adds the launches
@@ -182,6 +188,51 @@ int xmh_fast_table_check(const float *H, int L, int M, int T);
  * clip c of n_clips at out + c*frames*channels samples, id = clip0 + c. */
 int xmh_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips,
               int channels, int64_t frames, void *stream);
+
+/* ---------- backend table (one per backend) ------------------------------ */
+typedef struct XmhBackend {
+    const char *name;
+    int (*device_count)(void);
+    int (*set_device)(int dev);
+    int (*malloc)(void **p, size_t bytes);
+    void (*free)(void *p);
+    int (*host_alloc)(void **p, size_t bytes);
+    void (*host_free)(void *p);
+    int (*stream_create)(void **s);
+    void (*stream_destroy)(void *s);
+    int (*stream_sync)(void *s);
+    int (*memcpy_h2d)(void *dst, const void *src, size_t bytes, void *s);
+    int (*memcpy_d2h)(void *dst, const void *src, size_t bytes, void *s);
+    int (*memcpy_d2d)(void *dst, const void *src, size_t bytes, void *s);
+    int (*memset)(void *dst, int v, size_t bytes, void *s);
+    int (*memcpy2d)(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height,
+                    void *s);
+    int (*event_create)(void **e);
+    void (*event_destroy)(void *e);
+    int (*event_record)(void *e, void *s);
+    int (*event_elapsed)(float *ms, void *e0, void *e1);
+    int (*pointer_is_device)(const void *p);
+    int (*memcpy_peer)(void *dst, int dst_dev, const void *src, int src_dev, size_t bytes, void *s);
+    int (*comm_init_all)(void **comms, int n, const int *devs);
+    void (*comm_destroy)(void *comm);
+    int (*group_start)(void);
+    int (*group_end)(void);
+    int (*reduce_scatter_i32)(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s);
+    int (*comm_check)(void *comm);
+    const char *(*arch_name)(void);
+    int (*launch_mix)(const XmhMixJob *job, void *stream, int *n_launches, int *n_fast);
+    int (*launch_mix_window)(const XmhMixJob *job, void *stream, int *n_launches, int *n_fast);
+    int (*launch_fx)(const XmhFxJob *job, void *stream, int *n_launches);
+    int (*launch_mix_placed)(const XmhMixJob *job, void *stream, int *n_launches);
+    int (*launch_finish_s16)(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
+                             int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream);
+    int (*fast_table_check)(const float *H, int L, int M, int T);
+    int (*synth)(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips, int channels, int64_t frames,
+                 void *stream);
+} XmhBackend;
+extern const XmhBackend xmh_gpu;   /* csrc/xm_shim.hip (tests/host_asan: a CPU stand-in) */
+extern const XmhBackend xmh_cpu;   /* src/cpu/xm_cpu_backend.c */
+#define XMH_DEV_CPU (-1)           /* the host CPU backend's device ordinal */
 
 #ifdef __cplusplus
 }

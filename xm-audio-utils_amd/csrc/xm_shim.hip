@@ -2,13 +2,15 @@
 #include <stdlib.h>
 // xm_shim.hip — the thin C-ABI shim (SURVEY.md §1 layer L1): HIP runtime
 // wrappers with every hipError_t mapped to an XM_* status, and the kernel
-// dispatch for mix / effects jobs.  Only the C host layer (src/*.c) calls it.
+// dispatch for mix / effects jobs, collected into the gfx950 backend table
+// xmh_gpu (xm_shim.h).  Only the C host layer (src/*.c) reaches it, through
+// the xmh_* entry points (src/xm_backend.c).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 #include <mutex>
-#include "xm_shim.h"
+#include "xm_gpu.h"
 
 #define XM_EDEVICE_ (-1001)
 #define XM_ENOMEM_ (-12)
@@ -27,44 +29,39 @@ static inline int map_at(hipError_t e, int line)
 
 extern "C" {
 
-int xmh_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_launches);
-int xmh_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_launches);  // xm_resample_fast.hip
-int xmh_launch_fx_biquad(const XmhFxJob *j, void *stream);
-int xmh_launch_fx_fir(const XmhFxJob *j, void *stream);
-
-int xmh_device_count(void)
+int xmg_device_count(void)
 {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
 }
 
-int xmh_set_device(int dev) { return map(hipSetDevice(dev)); }
+int xmg_set_device(int dev) { return map(hipSetDevice(dev)); }
 
-int xmh_malloc(void **p, size_t bytes)
+int xmg_malloc(void **p, size_t bytes)
 {
     *p = nullptr;
     if (bytes == 0) bytes = 16;
     return map(hipMalloc(p, bytes));
 }
 
-void xmh_free(void *p)
+void xmg_free(void *p)
 {
     if (p) (void)hipFree(p);
 }
 
-int xmh_host_alloc(void **p, size_t bytes)
+int xmg_host_alloc(void **p, size_t bytes)
 {
     *p = nullptr;
     return map(hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocDefault));
 }
 
-void xmh_host_free(void *p)
+void xmg_host_free(void *p)
 {
     if (p) (void)hipHostFree(p);
 }
 
-int xmh_stream_create(void **s)
+int xmg_stream_create(void **s)
 {
     // a blocking stream: a handle's own stream is ordered after work the
     // caller queued on the legacy default stream (a memset or fill of the
@@ -75,24 +72,24 @@ int xmh_stream_create(void **s)
     return rc;
 }
 
-void xmh_stream_destroy(void *s)
+void xmg_stream_destroy(void *s)
 {
     if (s) (void)hipStreamDestroy((hipStream_t)s);
 }
 
-int xmh_stream_sync(void *s) { return map(hipStreamSynchronize((hipStream_t)s)); }
+int xmg_stream_sync(void *s) { return map(hipStreamSynchronize((hipStream_t)s)); }
 
-int xmh_memcpy_h2d(void *dst, const void *src, size_t n, void *s)
+int xmg_memcpy_h2d(void *dst, const void *src, size_t n, void *s)
 {
     return n ? map(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, (hipStream_t)s)) : 0;
 }
 
-int xmh_memcpy_d2h(void *dst, const void *src, size_t n, void *s)
+int xmg_memcpy_d2h(void *dst, const void *src, size_t n, void *s)
 {
     return n ? map(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, (hipStream_t)s)) : 0;
 }
 
-int xmh_memcpy_d2d(void *dst, const void *src, size_t n, void *s)
+int xmg_memcpy_d2d(void *dst, const void *src, size_t n, void *s)
 {
     return n ? map(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)s)) : 0;
 }
@@ -142,7 +139,7 @@ bool on_device(const void *p)
 
 extern "C" {
 
-int xmh_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height, void *s)
+int xmg_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t height, void *s)
 {
     if (!width || !height) return 0;
     const uintptr_t al = (uintptr_t)dst | (uintptr_t)src | dpitch | spitch | width;
@@ -162,12 +159,12 @@ int xmh_memcpy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_
     return map(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDefault, (hipStream_t)s));
 }
 
-int xmh_memset(void *dst, int v, size_t n, void *s)
+int xmg_memset(void *dst, int v, size_t n, void *s)
 {
     return n ? map(hipMemsetAsync(dst, v, n, (hipStream_t)s)) : 0;
 }
 
-int xmh_event_create(void **e)
+int xmg_event_create(void **e)
 {
     hipEvent_t h = nullptr;
     int rc = map(hipEventCreate(&h));
@@ -175,21 +172,21 @@ int xmh_event_create(void **e)
     return rc;
 }
 
-void xmh_event_destroy(void *e)
+void xmg_event_destroy(void *e)
 {
     if (e) (void)hipEventDestroy((hipEvent_t)e);
 }
 
-int xmh_event_record(void *e, void *s) { return map(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); }
+int xmg_event_record(void *e, void *s) { return map(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); }
 
-int xmh_event_elapsed(float *ms, void *e0, void *e1)
+int xmg_event_elapsed(float *ms, void *e0, void *e1)
 {
     int rc = map(hipEventSynchronize((hipEvent_t)e1));
     if (rc) return rc;
     return map(hipEventElapsedTime(ms, (hipEvent_t)e0, (hipEvent_t)e1));
 }
 
-int xmh_pointer_is_device(const void *p)
+int xmg_pointer_is_device(const void *p)
 {
     hipPointerAttribute_t a;
     memset(&a, 0, sizeof a);
@@ -201,7 +198,7 @@ int xmh_pointer_is_device(const void *p)
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ? 1 : 0;
 }
 
-int xmh_memcpy_peer(void *dst, int dst_dev, const void *src, int src_dev, size_t n, void *s)
+int xmg_memcpy_peer(void *dst, int dst_dev, const void *src, int src_dev, size_t n, void *s)
 {
     if (!n) return 0;
     if (dst_dev == src_dev) return map(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)s));
@@ -254,28 +251,28 @@ int cmap(ncclResult_t e, int line)
 }  // namespace
 extern "C" {
 
-int xmh_comm_init_all(void **comms, int n, const int *devs)
+int xmg_comm_init_all(void **comms, int n, const int *devs)
 {
     if (!rccl().ok) return XM_ECOMM_;
     return cmap(rccl().init_all((ncclComm_t *)comms, n, devs), __LINE__);
 }
 
-void xmh_comm_destroy(void *comm)
+void xmg_comm_destroy(void *comm)
 {
     if (comm && rccl().ok) (void)rccl().destroy((ncclComm_t)comm);
 }
 
-int xmh_group_start(void) { return rccl().ok ? cmap(rccl().group_start(), __LINE__) : XM_ECOMM_; }
-int xmh_group_end(void) { return rccl().ok ? cmap(rccl().group_end(), __LINE__) : XM_ECOMM_; }
+int xmg_group_start(void) { return rccl().ok ? cmap(rccl().group_start(), __LINE__) : XM_ECOMM_; }
+int xmg_group_end(void) { return rccl().ok ? cmap(rccl().group_end(), __LINE__) : XM_ECOMM_; }
 
-int xmh_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s)
+int xmg_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv_count, void *comm, void *s)
 {
     if (!rccl().ok) return XM_ECOMM_;
     return cmap(rccl().reduce_scatter(send, recv, recv_count, ncclInt32, ncclSum, (ncclComm_t)comm, (hipStream_t)s),
                 __LINE__);
 }
 
-int xmh_comm_check(void *comm)
+int xmg_comm_check(void *comm)
 {
     if (!rccl().ok || !comm) return XM_ECOMM_;
     ncclResult_t a = ncclSuccess;
@@ -297,7 +294,7 @@ int g_n_lds = 0;
 int g_cus[XMH_MAXDEV];   // 0: not read yet
 }  // namespace
 
-int xmh_cu_count(void)
+int xmg_cu_count(void)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= XMH_MAXDEV) return 256;
@@ -310,7 +307,7 @@ int xmh_cu_count(void)
     return g_cus[dev];
 }
 
-int xmh_func_lds(const void *kern, int bytes)
+int xmg_func_lds(const void *kern, int bytes)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return XM_EDEVICE_;
@@ -328,7 +325,7 @@ int xmh_func_lds(const void *kern, int bytes)
     return 0;
 }
 
-const char *xmh_arch_name(void)
+const char *xmg_arch_name(void)
 {
     static char name[64];
     int dev = 0;
@@ -338,31 +335,45 @@ const char *xmh_arch_name(void)
     return name;
 }
 
-int xmh_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
+int xmg_launch_mix(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
 {
-    int rc = xmh_launch_mix_fast(j, stream, n_launches);
+    int rc = xmg_launch_mix_fast(j, stream, n_launches);
     if (rc != XM_ENOSYS_) {   // fast path took it (or failed for real)
         if (!rc && n_fast) *n_fast += 1;
         return rc;
     }
-    return xmh_launch_mix_generic(j, stream, n_launches);
+    return xmg_launch_mix_generic(j, stream, n_launches);
 }
 
-int xmh_launch_mix_window(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
+int xmg_launch_mix_window(const XmhMixJob *j, void *stream, int *n_launches, int *n_fast)
 {
-    const int rc = xmh_launch_mix_fast(j, stream, n_launches);
+    const int rc = xmg_launch_mix_fast(j, stream, n_launches);
     if (!rc && n_fast) *n_fast += 1;
     return rc;
 }
 
-int xmh_launch_fx(const XmhFxJob *j, void *stream, int *n_launches)
+int xmg_launch_fx(const XmhFxJob *j, void *stream, int *n_launches)
 {
     int rc;
-    if (j->n_sos > 0) rc = xmh_launch_fx_biquad(j, stream);
-    else if (j->fir_len > 0) rc = xmh_launch_fx_fir(j, stream);
+    if (j->n_sos > 0) rc = xmg_launch_fx_biquad(j, stream);
+    else if (j->fir_len > 0) rc = xmg_launch_fx_fir(j, stream);
     else return 0;
     if (n_launches) *n_launches += 1;
     return rc;
 }
+
+// host side only: clang would otherwise promote this const table to the
+// device and link it against host functions there
+#ifndef __HIP_DEVICE_COMPILE__
+const XmhBackend xmh_gpu = {
+    "gfx950",
+    xmg_device_count, xmg_set_device, xmg_malloc, xmg_free, xmg_host_alloc, xmg_host_free,
+    xmg_stream_create, xmg_stream_destroy, xmg_stream_sync, xmg_memcpy_h2d, xmg_memcpy_d2h, xmg_memcpy_d2d,
+    xmg_memset, xmg_memcpy2d, xmg_event_create, xmg_event_destroy, xmg_event_record, xmg_event_elapsed,
+    xmg_pointer_is_device, xmg_memcpy_peer, xmg_comm_init_all, xmg_comm_destroy, xmg_group_start, xmg_group_end,
+    xmg_reduce_scatter_i32, xmg_comm_check, xmg_arch_name, xmg_launch_mix, xmg_launch_mix_window, xmg_launch_fx,
+    xmg_launch_mix_placed, xmg_launch_finish_s16, xmg_fast_table_check, xmg_synth,
+};
+#endif
 
 }  // extern "C"

@@ -1,9 +1,11 @@
 /*
  * xm_audio_mixer.c — the xm_audio_mixer_* C API (SURVEY.md §1 layers L3/L2):
  * validation, handle state, host<->device staging, batch strides, and the
- * dispatch into the HIP shim (csrc/xm_shim.h).  No arithmetic on samples
- * happens here: every sample is produced by a gfx950 kernel, and a handle
- * cannot be created without a usable GPU (no CPU fallback).
+ * dispatch into the compute backend (csrc/xm_shim.h).  No arithmetic on
+ * samples happens here: every sample is produced by a gfx950 kernel or, on a
+ * handle created with n_devices == 0, by the host CPU backend (src/cpu/).
+ * The backend is fixed at create time: a GPU handle without a usable GPU
+ * fails with XM_EDEVICE, it never falls back to the CPU.
  *
  * Build-owned API (reference has none: /root/reference/README.md:1);
  * contract in include/xm_audio_mixer.h and include/xm_audio_common.h.
@@ -103,7 +105,8 @@ static int cfg_valid(const XmMixerConfig *cfg)
 {
     return cfg && cfg->in_rate > 0 && cfg->out_rate > 0 && (cfg->channels == 1 || cfg->channels == 2) &&
            (cfg->sample_fmt == XM_FMT_S16 || cfg->sample_fmt == XM_FMT_F32) &&
-           (cfg->mem_kind == XM_MEM_HOST || cfg->mem_kind == XM_MEM_DEVICE) && cfg->device >= 0 &&
+           (cfg->mem_kind == XM_MEM_HOST || cfg->mem_kind == XM_MEM_DEVICE) &&
+           (cfg->device >= 0 || cfg->n_devices == 0) &&
            !(cfg->flags & ~(int32_t)(XM_MIXER_OUT_CONVERT | XM_MIXER_IN_CONVERT | XM_MIXER_PLANAR)) &&
            cfg->n_devices >= 0 &&
            cfg->n_devices <= XM_MAX_DEVICES;
@@ -157,7 +160,8 @@ XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status)
         for (int d = 0; d < cfg->n_devices; ++d) devs[d] = cfg->device + d;
         return xm_audio_mixer_create_multi(cfg, devs, cfg->n_devices, status);
     }
-    if (cfg->device >= xmh_device_count()) {
+    const int cpu = cfg->n_devices == 0;   /* n_devices 0 = the host CPU backend */
+    if (!cpu && cfg->device >= xmh_device_count()) {
         rc = XM_EDEVICE;
         goto out;
     }
@@ -167,7 +171,13 @@ XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status)
         goto out;
     }
     m->cfg = *cfg;
-    if ((rc = xmh_set_device(cfg->device))) goto out;
+    if (cpu) {
+        /* host memory is the CPU backend's device memory: HOST calls run in
+         * place, with no staging copies */
+        m->cfg.device = XMH_DEV_CPU;
+        m->cfg.mem_kind = XM_MEM_DEVICE;
+    }
+    if ((rc = xmh_set_device(m->cfg.device))) goto out;
     if ((rc = xm_table_build(&m->table, cfg->in_rate, cfg->out_rate))) goto out;
     if ((rc = xmh_stream_create(&m->own_stream))) goto out;
     m->stream = m->own_stream;
@@ -336,6 +346,7 @@ int xm_audio_mixer_set_stream(XmAudioMixer *m, void *s)
 {
     if (!m) return XM_EINVAL;
     if (m->multi) return XM_ENOSYS;   /* a HIP stream belongs to one device */
+    if (m->cfg.device == XMH_DEV_CPU) return XM_OK;   /* CPU calls are synchronous: nothing to order */
     m->stream = s ? s : m->own_stream;
     m->user_stream = s != NULL;
     return XM_OK;
@@ -394,6 +405,9 @@ static int upload_gains(XmAudioMixer *m)
     return rc;
 }
 
+static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *const *out, size_t n_out,
+                     const void *const **din, void *const **dout);
+
 /* Effects path (config 4): resample every track into scratch at unity gain,
  * run the chain on each track in place, then the no-resample mix with the
  * track gains.  Order per track: resample -> effects -> gain -> ordered sum. */
@@ -431,13 +445,26 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     r.out = scratch;
     r.out_ptrs = NULL;
     r.out_mix_stride = (int64_t)per_track;
+    const void **tp = NULL;   /* host table of the track pointers (irregular strides) */
     if (j0->in_ptrs) {
         r.in_ptrs = j0->in_ptrs;   /* same mix-major order */
-    } else if (j0->in_mix_stride == (int64_t)ntr * j0->in_track_stride) {
-        r.in_mix_stride = j0->in_track_stride;
+    } else if (j0->n_mix == 1 || j0->in_mix_stride == (int64_t)ntr * j0->in_track_stride) {
+        r.in_mix_stride = j0->in_track_stride;   /* track i of the flat list = mix i / ntr, track i % ntr */
         r.in_track_stride = 0;
     } else {
-        rc = XM_ENOSYS;   /* irregular strides with effects: use process_batch */
+        /* mixes not ntr tracks apart: every track of the batch through a table */
+        const int elem = in_bytes(m);
+        const void *const *din = NULL;
+        void *const *dummy = NULL;
+        tp = malloc(sizeof(void *) * ntot);
+        if (!tp) rc = XM_ENOMEM;
+        for (size_t i = 0; !rc && i < ntot; ++i)
+            tp[i] = (const char *)j0->in +
+                    ((int64_t)(i / (size_t)ntr) * j0->in_mix_stride + (int64_t)(i % (size_t)ntr) * j0->in_track_stride) *
+                        elem;
+        if (!rc) rc = ptr_table(m, tp, ntot, NULL, 0, &din, &dummy);
+        r.in_ptrs = din;
+        r.in_ptrs_host = tp;
     }
     if (!rc) rc = xmh_launch_mix(&r, m->stream, launches, &m->timing.fast_launches);
     /* 2) effects chain on every track, in insertion order */
@@ -496,6 +523,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     xmh_stream_sync(m->stream);
     xmh_free(tmp_ptrs);
     xmh_free(ug);
+    free(tp);
     return rc;
 }
 

@@ -78,9 +78,9 @@ int xm_synth_pcm(void *dst, int fmt, uint64_t seed, uint64_t clip0, int64_t n_cl
                  int64_t frames, int device, void *stream)
 {
     if (!dst || (fmt != XM_FMT_S16 && fmt != XM_FMT_F32) || n_clips < 0 || frames < 0 ||
-        (channels != 1 && channels != 2) || device < 0)
+        (channels != 1 && channels != 2) || (device < 0 && device != XM_DEVICE_CPU))
         return XM_EINVAL;
-    if (device >= xmh_device_count()) return XM_EDEVICE;
+    if (device != XM_DEVICE_CPU && device >= xmh_device_count()) return XM_EDEVICE;
     int rc = xmh_set_device(device);
     if (!rc) rc = xmh_synth(dst, fmt, seed, clip0, n_clips, channels, frames, stream);
     if (!rc && !stream) rc = xmh_stream_sync(NULL);

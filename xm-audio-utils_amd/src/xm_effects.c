@@ -54,11 +54,12 @@ XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status)
     int rc = XM_OK;
     XmEffects *e = NULL;
     if (!cfg || cfg->rate <= 0 || (cfg->channels != 1 && cfg->channels != 2) ||
-        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) || cfg->device < 0) {
+        (cfg->mem_kind != XM_MEM_HOST && cfg->mem_kind != XM_MEM_DEVICE) ||
+        (cfg->device < 0 && cfg->device != XM_DEVICE_CPU)) {
         rc = XM_EINVAL;
         goto out;
     }
-    if (cfg->device >= xmh_device_count()) {
+    if (cfg->device != XM_DEVICE_CPU && cfg->device >= xmh_device_count()) {
         rc = XM_EDEVICE;
         goto out;
     }
@@ -68,6 +69,7 @@ XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status)
         goto out;
     }
     e->cfg = *cfg;
+    if (cfg->device == XM_DEVICE_CPU) e->cfg.mem_kind = XM_MEM_DEVICE;   /* host memory is the CPU's: no staging */
     if ((rc = xmh_set_device(cfg->device))) goto out;
     if ((rc = xmh_stream_create(&e->own_stream))) goto out;
     e->stream = e->own_stream;
@@ -114,7 +116,8 @@ out:
 XmEffects *xm_effects_create(int rate, int channels, int n_devices)
 {
     XmEffectsConfig c = {rate, channels, XM_MEM_HOST, 0};
-    if (n_devices == 1) return xm_effects_create_ex(&c, NULL);
+    if (n_devices == 0) c.device = XM_DEVICE_CPU;   /* 0 = the host CPU backend */
+    if (n_devices <= 1) return xm_effects_create_ex(&c, NULL);
     if (n_devices < 1 || n_devices > XM_MAX_DEVICES) return NULL;
     int devs[XM_MAX_DEVICES];
     for (int d = 0; d < n_devices; ++d) devs[d] = d;
@@ -274,12 +277,14 @@ int xm_effects_set_stream(XmEffects *e, void *s)
 {
     if (!e) return XM_EINVAL;
     if (e->n_sub) return XM_ENOSYS;   /* one stream per device, owned by the sub-chains */
+    if (e->cfg.device == XM_DEVICE_CPU) return XM_OK;   /* CPU calls are synchronous */
     e->stream = s ? s : e->own_stream;
     e->user_stream = s != NULL;
     return XM_OK;
 }
 
-int xm_effects_device(const XmEffects *e) { return e && !e->n_sub ? e->cfg.device : -1; }
+/* the chain's device (XM_DEVICE_CPU for a CPU chain); a multi-device chain has none */
+int xm_effects_device(const XmEffects *e) { return e && !e->n_sub ? e->cfg.device : XM_DEVICE_NONE_; }
 
 XmEffects *xm_effects_clone_on(const XmEffects *src, int device, int *status)
 {

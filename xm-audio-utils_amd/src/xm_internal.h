@@ -35,6 +35,7 @@ typedef struct XmFxStage {
 } XmFxStage;
 
 int xm_effects_stages(const XmEffects *e, const XmFxStage **stages, int *n_stages);
+#define XM_DEVICE_NONE_ (-2)   /* xm_effects_device of a multi-device chain */
 int xm_effects_device(const XmEffects *e);
 /* the same chain (host coefficient copies replayed) on another device */
 XmEffects *xm_effects_clone_on(const XmEffects *src, int device, int *status);

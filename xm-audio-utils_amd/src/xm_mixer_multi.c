@@ -92,7 +92,7 @@ XmMulti *xm_multi_create(const XmMixerConfig *cfg, const int *devs, int n, int *
     }
     mu->n = n;
     mu->cfg = *cfg;
-    mu->cfg.n_devices = 0;
+    mu->cfg.n_devices = 1;   /* each sub-handle: one GPU */
     mu->distinct = 1;
     for (int d = 0; d < n; ++d) {
         mu->devs[d] = devs[d];

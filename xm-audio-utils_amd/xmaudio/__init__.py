@@ -39,6 +39,7 @@ _lib = C.CDLL(LIB_PATH)
 XM_OK, XM_EINVAL, XM_ENOMEM, XM_EDEVICE, XM_ECOMM, XM_ENOSYS = 0, -22, -12, -1001, -1002, -1003
 XM_FMT_S16, XM_FMT_F32 = 1, 2
 XM_MEM_HOST, XM_MEM_DEVICE = 0, 1
+XM_DEVICE_CPU = -1   # the host CPU backend (include/xm_audio_common.h)
 XM_MIXER_OUT_CONVERT = 1
 XM_MIXER_IN_CONVERT = 2
 XM_MIXER_PLANAR = 4
@@ -191,9 +192,14 @@ def out_frames(in_rate: int, out_rate: int, n: int) -> int:
     return _lib.xm_resample_out_frames(in_rate, out_rate, n)
 
 
+def _dev(device) -> int:
+    """device ordinal: an int (HIP device) or "cpu" (XM_DEVICE_CPU)"""
+    return XM_DEVICE_CPU if device == "cpu" else int(device)
+
+
 def synth(ptr: int, fmt: str, seed: int, clip0: int, n_clips: int, channels: int, frames: int,
-          device: int = 0, stream: int | None = None):
-    _check(_lib.xm_synth_pcm(ptr, FMT[fmt], seed, clip0, n_clips, channels, frames, device, stream),
+          device: int | str = 0, stream: int | None = None):
+    _check(_lib.xm_synth_pcm(ptr, FMT[fmt], seed, clip0, n_clips, channels, frames, _dev(device), stream),
            "xm_synth_pcm")
 
 
@@ -223,14 +229,18 @@ class Mixer:
     """xm_audio_mixer_* handle."""
 
     def __init__(self, in_rate: int, out_rate: int, channels: int = 2, fmt: str = "f32",
-                 mem: str = "host", device: int = 0, convert_out: bool = False, devices=None,
-                 n_devices: int = 0, convert_in: bool = False, planar: bool = False):
-        """devices: a device list -> multi-device handle (xm_audio_mixer_create_multi);
-        n_devices > 1: devices device .. device+n-1 (XmMixerConfig.n_devices).
+                 mem: str = "host", device: int | str = 0, convert_out: bool = False, devices=None,
+                 n_devices: int = 1, convert_in: bool = False, planar: bool = False):
+        """device: a HIP device ordinal, or "cpu" for the host CPU backend
+        (XmMixerConfig.n_devices = 0); devices: a device list -> multi-device
+        handle (xm_audio_mixer_create_multi); n_devices > 1: devices
+        device .. device+n-1 (XmMixerConfig.n_devices; 0 = the CPU backend).
         convert_in: tracks in the other sample format (XM_MIXER_IN_CONVERT);
         planar: planar PCM (XM_MIXER_PLANAR), arrays [..., channels, frames]."""
         flags = ((XM_MIXER_OUT_CONVERT if convert_out else 0) | (XM_MIXER_IN_CONVERT if convert_in else 0) |
                  (XM_MIXER_PLANAR if planar else 0))
+        if device == "cpu":
+            device, n_devices = 0, 0
         cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device, flags, n_devices)
         st = C.c_int(0)
         if devices is not None:
@@ -241,6 +251,8 @@ class Mixer:
         if not self._h:
             raise XmError(st.value, "xm_audio_mixer_create")
         self.cfg = cfg
+        self.backend = "cpu" if n_devices == 0 and devices is None else "gpu"
+        self.fused = int(self.backend == "gpu")   # launches of the fused gfx950 kernel a fused-shape call makes
         self.fmt = FMT[fmt]
         other = np.float32 if self.fmt == XM_FMT_S16 else np.int16
         self.dtype = other if convert_in else DTYPE[self.fmt]          # input tracks
@@ -408,9 +420,10 @@ class Mixer:
 class Effects:
     """xm_effects_* handle."""
 
-    def __init__(self, rate: int, channels: int = 2, mem: str = "host", device: int = 0, devices=None):
-        """devices: a device list -> multi-device chain (xm_effects_create_multi)."""
-        cfg = XmEffectsConfig(rate, channels, MEM[mem], device)
+    def __init__(self, rate: int, channels: int = 2, mem: str = "host", device: int | str = 0, devices=None):
+        """device: a HIP device ordinal, or "cpu" (XM_DEVICE_CPU, the host CPU
+        backend); devices: a device list -> multi-device chain (xm_effects_create_multi)."""
+        cfg = XmEffectsConfig(rate, channels, MEM[mem], _dev(device))
         st = C.c_int(0)
         if devices is not None:
             dl = (C.c_int * len(devices))(*devices)
