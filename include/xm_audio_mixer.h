@@ -137,7 +137,10 @@ XM_API int xm_audio_mixer_set_track_effects(XmAudioMixer *m, const struct XmEffe
 /* Output frames per mix for a given input length. */
 XM_API size_t xm_audio_mixer_out_frames(const XmAudioMixer *m, size_t frames_in);
 
-/* Install a caller-owned hipStream_t (NULL restores the handle's own stream). */
+/* Install a caller-owned hipStream_t (NULL restores the handle's own stream).
+ * The handle's own stream is a blocking stream (hipStreamDefault): its work is
+ * ordered after what the caller queued on the legacy default stream (a
+ * memset or fill of the buffers) and the other way round, on that device. */
 XM_API int xm_audio_mixer_set_stream(XmAudioMixer *m, void *hip_stream);
 
 /* in  : batch*n_tracks pointers, mix-major: in[b*n_tracks + tr]

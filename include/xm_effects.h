@@ -37,13 +37,14 @@ typedef struct XmEffectsConfig {
     int32_t rate;        /* Hz */
     int32_t channels;    /* 1 or 2 */
     int32_t mem_kind;    /* XmMemKind of in/out pointers */
-    int32_t device;      /* HIP device ordinal */
+    int32_t device;      /* HIP device ordinal, or XM_DEVICE_CPU (the host CPU backend) */
 } XmEffectsConfig;
 
 XM_API XmEffects *xm_effects_create_ex(const XmEffectsConfig *cfg, int *status);
-/* Host-memory chain (SURVEY.md §8(b) form): n_devices == 1 on device 0,
- * n_devices > 1 over devices 0 .. n_devices-1 (xm_effects_create_multi);
- * NULL if n_devices is out of [1, 16] or names a device that is not there. */
+/* Host-memory chain (SURVEY.md §8(b) form): n_devices == 0 on the host CPU
+ * backend (XM_DEVICE_CPU), n_devices == 1 on GPU 0, n_devices > 1 over GPUs
+ * 0 .. n_devices-1 (xm_effects_create_multi); NULL if n_devices is out of
+ * [0, 16] or names a device that is not there. */
 XM_API XmEffects *xm_effects_create(int rate, int channels, int n_devices);
 
 /* Multi-device chain over an explicit device list (n_devices in [1, 16]; a
@@ -56,7 +57,9 @@ XM_API XmEffects *xm_effects_create(int rate, int channels, int n_devices);
  * one-device result bit for bit.  With XM_MEM_DEVICE, block d's pointers must
  * be on device d.  cfg->device is ignored; set_stream returns XM_ENOSYS.
  * Such a chain attaches to multi-device mixers (copied per device), not to a
- * single-device mixer (XM_EINVAL there). */
+ * single-device mixer (XM_EINVAL there).  A list of one device returns the
+ * plain single-device chain on it.  An effect that cannot be added to every
+ * device's chain is added to none. */
 XM_API XmEffects *xm_effects_create_multi(const XmEffectsConfig *cfg, const int *devices, int n_devices,
                                           int *status);
 
@@ -79,6 +82,9 @@ XM_API int xm_effects_add_fir(XmEffects *e, const float *h, int K);
 XM_API int xm_effects_count(const XmEffects *e);
 XM_API int xm_effects_get_biquad(const XmEffects *e, int index, float sos[6]);
 
+/* Install a caller-owned hipStream_t (NULL: the chain's own stream, which is
+ * created blocking: ordered after the legacy default stream's work, as a
+ * synchronous caller expects).  A CPU chain accepts and ignores it. */
 XM_API int xm_effects_set_stream(XmEffects *e, void *hip_stream);
 
 /* in/out: batch pointers of frames*channels float32 samples (in == out allowed). */

@@ -4,7 +4,8 @@
 Runs bench.py once per variant, each in its own process, and prints ms/step:
   base        product library (lib/)
   abl<N>      lib_ablate/ build (`make ablate`), XM_FAST_ABLATE=N:
-              1 no DMA/copies, 16 cycle attribution (8 waves per workgroup,
+              1 no DMA/copies, 2 no taps, 4 no exchange / track sum,
+              8 constant gains, 16 cycle attribution (8 waves per workgroup,
               as the product)
 Ablated variants compute wrong results on purpose; only their time matters.
 usage: python tools/ablate.py [variant ...]
@@ -19,7 +20,7 @@ ABL_LIB = os.path.join(ROOT, "xm-audio-utils_amd", "lib_ablate", "libxm_audio.so
 VARIANTS = {
     "base": {},
 }
-for n in (1, 16):
+for n in (1, 2, 4, 8, 16):
     VARIANTS[f"abl{n}"] = {"XM_AUDIO_LIB": ABL_LIB, "XM_FAST_ABLATE": str(n)}
 
 

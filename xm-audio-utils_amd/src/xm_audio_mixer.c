@@ -897,6 +897,14 @@ static int64_t st_direct_cut(const XmAudioMixer *m, int64_t B0, int64_t R, int64
     const int64_t q = (B0 + 32 + M - 1) / M;   /* first SP whose input frame a0 = q*M has its lead-in in the block */
     if (q * L > ob_al) ob_al = q * L;
     if (mend - ob_al < 4 * L || ob_al / L * M >= R) return -1;
+    /* step 3 moves the frames the next release needs, [w0, R), from the
+     * caller's block into the window, which holds at least the frames kept
+     * plus the head's part of the block: decide here, before any launch,
+     * that they fit (else the window path) */
+    int64_t w0 = st_first_needed(m, mend) - 32;
+    if (w0 > R) w0 = R;
+    const int64_t held = (m->st_recv - m->st_w0) + (ob_al / L * M + 16 - B0);
+    if (w0 >= B0 && R - w0 > held) return -1;
     return ob_al;
 }
 
@@ -1043,7 +1051,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
          * needs, [w0, R), come from the caller's block */
         const size_t left = (size_t)(R - w0);
         char *nwin = (char *)m->st_win[m->st_cur ^ 1];
-        if (left > m->st_cap) return XM_EINVAL;   /* cannot happen: w0 >= R - 32 - T - M/L */
+        if (left > m->st_cap) return XM_EINVAL;   /* excluded by st_direct_cut before any launch */
         if (ms == (ptrdiff_t)ntr * ts || batch == 1)
             rc = xmh_memcpy2d(nwin, pitch, (const char *)in + (size_t)(w0 - B0) * fb, (size_t)ts * (size_t)elem,
                               left * fb, rows, m->stream);

@@ -93,6 +93,11 @@ XmEffects *xm_effects_create_multi(const XmEffectsConfig *cfg, const int *device
             rc = XM_EDEVICE;
             goto out;
         }
+    if (n_devices == 1) {   /* one device: the plain single-device chain (set_stream, single-device mixers) */
+        XmEffectsConfig c = *cfg;
+        c.device = devices[0];
+        return xm_effects_create_ex(&c, status);
+    }
     e = calloc(1, sizeof *e);
     if (!e) {
         rc = XM_ENOMEM;
@@ -176,6 +181,19 @@ void xm_effects_freep(XmEffects **pe)
     *pe = NULL;
 }
 
+/* undo the effect just added to sub-chains 0 .. n-1 of a multi-device chain */
+static void drop_last(XmEffects *e, int n)
+{
+    for (int d = 0; d < n; ++d) {
+        XmEffects *s = e->sub[d];
+        if (s->n_effects == 0) continue;
+        s->n_effects--;
+        free(s->fx[s->n_effects].fir);
+        s->fx[s->n_effects].fir = NULL;
+        s->dirty = 1;
+    }
+}
+
 int xm_effects_add_biquad(XmEffects *e, const float sos[6])
 {
     if (!e || !sos) return XM_EINVAL;
@@ -186,7 +204,10 @@ int xm_effects_add_biquad(XmEffects *e, const float sos[6])
     /* a cascade longer than XM_MAX_SOS sections is split by the stager */
     for (int d = 0; d < e->n_sub; ++d) {   /* multi-device: every device's chain */
         const int rc = xm_effects_add_biquad(e->sub[d], sos);
-        if (rc) return rc;
+        if (rc) {
+            drop_last(e, d);   /* every device keeps the same chain */
+            return rc;
+        }
     }
     e->fx[e->n_effects].kind = 1;
     memcpy(e->fx[e->n_effects].sos, sos, sizeof(float) * 6);
@@ -249,12 +270,16 @@ int xm_effects_add_fir(XmEffects *e, const float *h, int K)
 {
     if (!e || !h || K < 1 || K > XM_MAX_FIR) return XM_EINVAL;
     if (e->n_effects >= XM_MAX_EFFECTS) return XM_ENOMEM;
+    float *c = malloc(sizeof(float) * (size_t)K);   /* the parent's copy first: nothing to undo if it fails */
+    if (!c) return XM_ENOMEM;
     for (int d = 0; d < e->n_sub; ++d) {   /* multi-device: every device's chain */
         const int rc = xm_effects_add_fir(e->sub[d], h, K);
-        if (rc) return rc;
+        if (rc) {
+            drop_last(e, d);   /* every device keeps the same chain */
+            free(c);
+            return rc;
+        }
     }
-    float *c = malloc(sizeof(float) * (size_t)K);
-    if (!c) return XM_ENOMEM;
     memcpy(c, h, sizeof(float) * (size_t)K);
     e->fx[e->n_effects].kind = 2;
     e->fx[e->n_effects].n = K;
@@ -325,8 +350,18 @@ static int build_stages(XmEffects *e)
         } else {
             s->kind = 2;
             s->n = e->fx[i].n;
-            rc = xmh_malloc((void **)&s->coef_dev, sizeof(float) * (size_t)s->n);
-            if (!rc) rc = xmh_memcpy_h2d(s->coef_dev, e->fx[i].fir, sizeof(float) * (size_t)s->n, e->stream);
+            /* at least 16 floats, zero past the taps: the FIR kernel loads
+             * coefficients in 14-tap blocks (csrc/xm_fx.hip k_fir_rb) */
+            const size_t nc = s->n < 16 ? 16 : (size_t)s->n;
+            float *hc = calloc(nc, sizeof(float));
+            if (!hc) rc = XM_ENOMEM;
+            if (!rc) {
+                memcpy(hc, e->fx[i].fir, sizeof(float) * (size_t)s->n);
+                rc = xmh_malloc((void **)&s->coef_dev, sizeof(float) * nc);
+            }
+            if (!rc) rc = xmh_memcpy_h2d(s->coef_dev, hc, sizeof(float) * nc, e->stream);
+            if (!rc) rc = xmh_stream_sync(e->stream);   /* hc is pageable host memory */
+            free(hc);
             ++i;
         }
         if (!rc) e->n_stages++;
