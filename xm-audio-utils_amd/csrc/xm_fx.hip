@@ -4,11 +4,13 @@
 // Biquad: scipy sosfilt order (transposed DF-II, _signaltools.py:4601),
 // sections in order, state zero at clip start.  The recurrence is serial in
 // time, so exactness (SURVEY.md §7 hard part 3) limits the parallelism to
-// clips x sections x channels: k_biquad_lane (cascades of up to 16
-// sections) gives each (clip, section, channel) its own lane, k_biquad_pipe
-// (longer cascades) each (clip, section) with stereo packed; both chain the
-// sections through LDS (see the comments at the kernels).
-// FIR: upfirdn order (_upfirdn.py:107), taps staged in LDS, input tile in LDS.
+// clips x sections x channels: k_biquad_pc (cascades of up to 16 sections)
+// gives each (clip, section, channel) its own lane on a chain wave fed by a
+// producer wave, k_biquad_pipe (longer cascades) each (clip, section) with
+// stereo packed; both chain the sections through LDS (see the comments at the
+// kernels).  Earlier designs (k_biquad_lane, the LDS-tap FIR k_fir) and their
+// dev switches left the product in round 4; git history keeps them.
+// FIR: upfirdn order (_upfirdn.py:107), register-blocked over an LDS tile.
 #include <stdlib.h>
 #include <algorithm>
 #include "xm_device.h"
@@ -109,10 +111,6 @@ constexpr int BQ_KPW = 16;   // clips per wave at most (16 DMA + 16 stores per s
 constexpr int BQ_RP = 80;    // granules per input / output row: 65 + up to 15 of bank skew
 constexpr size_t BQ_LDS = ((size_t)4 * BQ_KPW * BQ_RP + 64 * (BQ_G + 1)) * 16;   // 148,480 B
 
-#ifdef XM_BQ_PROF
-__device__ uint64_t g_bq_prof[4096];   // dev: per-workgroup cycles (compute wave: chunk, barrier wait)
-__device__ uint32_t g_bq_hw[2048];     // dev: HW_ID of each k_biquad_pc wave
-#endif
 
 // The copy wave shared by both biquad kernels: every HBM access of the
 // workgroup.  inb_row(p, k) / outb_row(p, k) give the LDS granule (16 B) where
@@ -302,15 +300,8 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
     const int kc = min(kk, BQ_KPW - 1);
     const bq_f4 *srow = &sec[(lane + 63) & 63][0];
     const bool last = s == ns - 1 && valid;        // idle lanes write their own (unread) sec row
-#ifdef XM_BQ_PROF
-    uint64_t pr[2] = {0, 0}, tq = __builtin_amdgcn_s_memtime();
-#define XM_BQ_T(n) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pr[n] += t_ - tq; tq = t_; } while (0)
-#else
-#define XM_BQ_T(n) do { } while (0)
-#endif
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        XM_BQ_T(1);
         const int64_t c = i - s;                   // chunk this lane filters
         // every lane runs the chunk (uniform control flow); a lane outside its
         // chunk range keeps its state and its outputs are never stored
@@ -354,280 +345,27 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
             dst[g] = r;
         }
         if (!act) { z0 = z0s; z1 = z1s; }
-        XM_BQ_T(0);
         __syncthreads();                           // chunk i + 1 staged; outputs visible to the copy wave
     }
-#ifdef XM_BQ_PROF
-    if (lane == 0 && blockIdx.x < 2048)
-        for (int n = 0; n < 2; ++n) g_bq_prof[blockIdx.x * 2 + n] = pr[n];
-#endif
-#undef XM_BQ_T
     if (ST && st) {
         if constexpr (C == 2) { st[0] = z0.x; st[1] = z0.y; st[2] = z1.x; st[3] = z1.y; }
         else { st[0] = z0; st[1] = z1; }
     }
 }
 
-// ---- one recurrence per lane: k_biquad_lane ---------------------------------
-// Lane = (clip k, section s, channel ch), scalar fp32 (no packing).  Per lane
-// and frame this is the packed kernel's 9 VALU ops, but every lane moves
-// only 4 B in and 4 B out of LDS per frame (ds_read2_b32 / ds_write2_b32 on
-// the interleaved chunk) instead of 8 + 8: the LDS store transfer (2 cycles
-// per dword, at half rate for a lone wave, MI355X_MICROARCH.md §LDS) was a
-// third of the packed compute wave's time.  Twice the waves, each ~25 %
-// faster per frame; only 1/6 of the SIMDs are busy either way.
-// Lane = 4*blk + r, blk = grp*ns + s; a group is 4/C clips (r = ci*C + ch),
-// so a workgroup holds (16 / ns) * 4 / C clips (cascades of up to 16
-// sections; longer ones take k_biquad_pipe).  Chunks, steps, the copy wave
-// and the per-step barrier are k_biquad_pipe's.
-// LDS rows (floats, BQ_LN_RS apart): inb[p][k], outb[p][k] (DMA / store
-// rows, 16-B aligned) and sec[k][s] (section s's output chunk of clip k),
-// each chunk interleaved as in HBM.  A row's base is skewed to the bank
-// slot (block & 7) * 4 (+ ci*C for sec rows) of the block that reads it, so
-// the 32 lanes of each half-wave access 32 distinct banks (sec rows are
-// written by the block before, which lands on the next slot: distinct too).
-// Lanes with no clip use the spare last row.
-//
-// MF (dev A/B only, -DXM_BQ_MF): the three feed-forward products b_r * x on
-// the matrix core, one v_mfma_f32_4x4x1_16b_f32 per frame (block lane r
-// supplies row r of A = b0, b1, b2, 0 of the block's section, every lane its
-// own x as B, D = A*B + (-0)), leaving 6 VALU ops per frame.  Measured
-// 12.1 ms vs 14.2 for k_biquad_pipe on config 4, but NOT exact: the MFMA
-// flushes denormal products and does not keep IEEE signed zeros
-// (tools/ubench/bq_mfma.hip: 1948 value and 45866 zero-sign mismatches in
-// 16.8M products), so silence and decaying tails would differ from sosfilt.
-constexpr int BQ_LN_RS = 288;                      // floats per row: 256 + 32 of skew
-constexpr int BQ_LN_ROWS = 128;                    // 2 x 16 inb + 2 x 16 outb + 64 sec
-static_assert((size_t)BQ_LN_RS * BQ_LN_ROWS * 4 <= BQ_LDS, "rows fit the launch's LDS");
-
-// two frames (a, b) of one chain, products on the VALU, in bq_step2's order
-// (each dependent op one instruction behind its producer)
-__device__ __forceinline__ __attribute__((unused)) void bq_lane_pair(float xa, float xb, float &z0, float &z1, float b0, float b1, float b2,
-                                             float na1, float na2, float &oa, float &ob)
-{
-    float p0, p1, p2, t, u;
-    asm volatile(
-        "v_mul_f32 %[p0], %[b0], %[xa]\n\t"
-        "v_mul_f32 %[p1], %[b1], %[xa]\n\t"
-        "v_add_f32 %[oa], %[z0], %[p0]\n\t"
-        "v_mul_f32 %[p2], %[b2], %[xa]\n\t"
-        "v_mul_f32 %[t], %[na1], %[oa]\n\t"
-        "v_mul_f32 %[p0], %[b0], %[xb]\n\t"
-        "v_add_f32 %[t], %[p1], %[t]\n\t"
-        "v_mul_f32 %[u], %[na2], %[oa]\n\t"
-        "v_add_f32 %[z0], %[z1], %[t]\n\t"
-        "v_add_f32 %[z1], %[p2], %[u]\n\t"
-        "v_add_f32 %[ob], %[z0], %[p0]\n\t"
-        "v_mul_f32 %[p1], %[b1], %[xb]\n\t"
-        "v_mul_f32 %[t], %[na1], %[ob]\n\t"
-        "v_mul_f32 %[p2], %[b2], %[xb]\n\t"
-        "v_add_f32 %[t], %[p1], %[t]\n\t"
-        "v_mul_f32 %[u], %[na2], %[ob]\n\t"
-        "v_add_f32 %[z0], %[z1], %[t]\n\t"
-        "v_add_f32 %[z1], %[p2], %[u]"
-        : [oa] "=&v"(oa), [ob] "=&v"(ob), [p0] "=&v"(p0), [p1] "=&v"(p1), [p2] "=&v"(p2), [t] "=&v"(t),
-          [u] "=&v"(u), [z0] "+v"(z0), [z1] "+v"(z1)
-        : [xa] "v"(xa), [xb] "v"(xb), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [na1] "v"(na1), [na2] "v"(na2));
-}
-
-// MF: two frames from precomputed products (z1 alternates with w: no move)
-__device__ __forceinline__ __attribute__((unused)) void bq_mf_pair(const float (&pa)[4], const float (&pb)[4], float &z0, float &z1, float na1,
-                                           float na2, float &oa, float &ob)
-{
-    float t, u, w;
-    asm volatile(
-        "v_add_f32 %[oa], %[z0], %[pa0]\n\t"
-        "v_mul_f32 %[t], %[na1], %[oa]\n\t"
-        "v_mul_f32 %[u], %[na2], %[oa]\n\t"
-        "v_add_f32 %[t], %[pa1], %[t]\n\t"
-        "v_add_f32 %[w], %[pa2], %[u]\n\t"
-        "v_add_f32 %[z0], %[z1], %[t]\n\t"
-        "v_add_f32 %[ob], %[z0], %[pb0]\n\t"
-        "v_mul_f32 %[t], %[na1], %[ob]\n\t"
-        "v_mul_f32 %[u], %[na2], %[ob]\n\t"
-        "v_add_f32 %[t], %[pb1], %[t]\n\t"
-        "v_add_f32 %[z1], %[pb2], %[u]\n\t"
-        "v_add_f32 %[z0], %[w], %[t]"
-        : [oa] "=&v"(oa), [ob] "=&v"(ob), [t] "=&v"(t), [u] "=&v"(u), [w] "=&v"(w), [z0] "+v"(z0), [z1] "+v"(z1)
-        : [pa0] "v"(pa[0]), [pa1] "v"(pa[1]), [pa2] "v"(pa[2]), [pb0] "v"(pb[0]), [pb1] "v"(pb[1]), [pb2] "v"(pb[2]),
-          [na1] "v"(na1), [na2] "v"(na2));
-}
-
-template <int C, bool ST, bool MF = false>
-__global__ __launch_bounds__(128) void k_biquad_lane(XmhFxJob j)
-{
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    constexpr int FPL = 4 / C;
-    constexpr int CH = BQ_G * FPL;                 // frames per chunk
-    constexpr int NQ = CH / 4;                     // quads (4 frames of one channel) per chunk
-    constexpr int CPG = 4 / C;                     // clips per group
-    extern __shared__ bq_f4 bq_lds[];
-    float *lf = (float *)bq_lds;
-    const int ns = j.n_sos;
-    const int gpw = 16 / ns;                       // groups per wave
-    const int kpw = min(gpw * CPG, BQ_KPW);        // clips per workgroup
-    const int clip0 = blockIdx.x * kpw;
-    const int nclip = min(kpw, j.n_clips - clip0);
-    const int64_t N = j.frames;
-    const int64_t nchunk = (N + CH - 1) / CH;
-    const int64_t steps = nchunk + ns - 1;
-    // row bases (floats); the slot of clip k's section-s block is ((k / CPG) * ns + s) & 7
-    auto slot = [=](int k, int s) __attribute__((always_inline)) { return (((k / CPG) * ns + s) & 7) * 4; };
-    auto inb_f = [=](int p, int k) __attribute__((always_inline)) { return (p * 16 + k) * BQ_LN_RS + slot(k, 0); };
-    auto outb_f = [=](int p, int k) __attribute__((always_inline)) {
-        return (32 + p * 16 + k) * BQ_LN_RS + slot(k, ns);
-    };
-    auto sec_f = [=](int k, int s) __attribute__((always_inline)) {   // read by section s + 1
-        return (64 + k * ns + s) * BQ_LN_RS + slot(k, s + 1) + (k % CPG) * C;
-    };
-
-    if (threadIdx.x >= 64) {
-        bq_copy_wave<C>(j, clip0, nclip, steps, ns, [=](int p, int k) { return inb_f(p, k) / 4; },
-                        [=](int p, int k) { return outb_f(p, k) / 4; });
-        return;
-    }
-
-    const int lane = threadIdx.x & 63;
-    const int blk = lane >> 2, r = lane & 3;
-    const int grp = blk / ns, s = blk % ns, ci = r / C, ch = r % C;
-    const int kk = grp * CPG + ci;
-    const bool valid = blk < gpw * ns && kk < nclip;
-    const float *q = j.sos + 6 * s;
-    const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
-    const float na1 = -a1, na2 = -a2;              // (-a)*o == -(a*o): IEEE negation is exact
-    [[maybe_unused]] const float A = r < 3 ? q[r] : 0.0f;   // MF: row r of the block's A
-    float z0 = 0.0f, z1 = 0.0f;
-    float *st = (ST && valid) ? j.state + ((size_t)(clip0 + kk) * ns + s) * 2 * C : nullptr;
-    if (ST && st) {
-        z0 = st[ch];
-        z1 = st[C + ch];
-    }
-    const bool last = s == ns - 1;
-    const int spare = (BQ_LN_ROWS - 1) * BQ_LN_RS + (lane & 31) - ch;   // + ch below: within the row
-    const int src_sec = valid ? (s ? sec_f(kk, s - 1) : -1) : spare;
-    const int dst_row = valid ? (last ? -1 : sec_f(kk, s)) : spare;
-#ifdef XM_BQ_PROF
-    uint64_t pr[2] = {0, 0}, tq = __builtin_amdgcn_s_memtime();
-#define XM_BQ_T(n) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pr[n] += t_ - tq; tq = t_; } while (0)
-#else
-#define XM_BQ_T(n) do { } while (0)
-#endif
-    __syncthreads();
-    for (int64_t i = 0; i < steps; ++i) {
-        XM_BQ_T(1);
-        const int64_t c = i - s;                   // chunk this lane filters
-        // every lane runs the chunk (uniform control flow); a lane outside its
-        // chunk range keeps its state and its outputs are never used
-        const bool act = valid && c >= 0 && c < nchunk;
-        const float z0s = z0, z1s = z1;
-        const int par = (int)(i & 1);
-        const float *src = lf + (src_sec >= 0 ? src_sec : inb_f(par, kk)) + ch;
-        float *dst = lf + (dst_row >= 0 ? dst_row : outb_f(par, kk)) + ch;
-        const bool tail = ST && st && act && (c + 1) * CH > N;
-        if (__builtin_amdgcn_ballot_w64(tail) != 0) {
-            // a streamed block's last chunk: frames past N are padding and must
-            // not advance the state (wave-uniform branch)
-            for (int f = 0; f < CH; ++f) {
-                const float v = src[f * C];
-                const float o = b0 * v + z0;
-                if (!(tail && c * CH + f >= N)) {
-                    z0 = (b1 * v - a1 * o) + z1;
-                    z1 = b2 * v - a2 * o;
-                }
-                dst[f * C] = o;
-            }
-        } else if constexpr (!MF) {
-            // quads: x of quad qd + 2 is read while quad qd is filtered (before
-            // the left neighbour's writes of this step reach it)
-            float xa[4], xb[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) xa[e] = src[e * C];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) xb[e] = src[(4 + e) * C];
-#pragma unroll
-            for (int qd = 0; qd < NQ; ++qd) {
-                float xn[4];
-                if (qd + 2 < NQ) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) xn[e] = src[(4 * (qd + 2) + e) * C];
-                }
-                float o[4];
-                bq_lane_pair(xa[0], xa[1], z0, z1, b0, b1, b2, na1, na2, o[0], o[1]);
-                bq_lane_pair(xa[2], xa[3], z0, z1, b0, b1, b2, na1, na2, o[2], o[3]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) dst[(4 * qd + e) * C] = o[e];
-                asm volatile("" ::: "memory");     // later quads' reads stay behind these writes
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    xa[e] = xb[e];
-                    if (qd + 2 < NQ) xb[e] = xn[e];
-                }
-            }
-        } else {
-            const f4v nz = {-0.0f, -0.0f, -0.0f, -0.0f};
-            float xb[4];
-            float P[2][4][4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const f4v d = __builtin_amdgcn_mfma_f32_4x4x1f32(A, src[e * C], nz, 0, 0, 0);
-                P[0][e][0] = d[0]; P[0][e][1] = d[1]; P[0][e][2] = d[2];
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) xb[e] = src[(4 + e) * C];
-#pragma unroll
-            for (int qd = 0; qd < NQ; ++qd) {
-                const int cb = qd & 1;
-                float xn[4];
-                if (qd + 2 < NQ) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) xn[e] = src[(4 * (qd + 2) + e) * C];
-                }
-                if (qd + 1 < NQ) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const f4v d = __builtin_amdgcn_mfma_f32_4x4x1f32(A, xb[e], nz, 0, 0, 0);
-                        P[cb ^ 1][e][0] = d[0]; P[cb ^ 1][e][1] = d[1]; P[cb ^ 1][e][2] = d[2];
-                    }
-                }
-                float o[4];
-                bq_mf_pair(P[cb][0], P[cb][1], z0, z1, na1, na2, o[0], o[1]);
-                bq_mf_pair(P[cb][2], P[cb][3], z0, z1, na1, na2, o[2], o[3]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) dst[(4 * qd + e) * C] = o[e];
-                asm volatile("" ::: "memory");
-                if (qd + 2 < NQ) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) xb[e] = xn[e];
-                }
-            }
-        }
-        if (!act) { z0 = z0s; z1 = z1s; }
-        XM_BQ_T(0);
-        __syncthreads();                           // chunk i + 1 staged; outputs visible to the copy wave
-    }
-#ifdef XM_BQ_PROF
-    if (lane == 0 && blockIdx.x < 2048)
-        for (int n = 0; n < 2; ++n) g_bq_prof[blockIdx.x * 2 + n] = pr[n];
-#endif
-#undef XM_BQ_T
-    if (ST && st) {
-        st[ch] = z0;
-        st[C + ch] = z1;
-    }
-}
-
 // ---- producer / chain split: k_biquad_pc ------------------------------------
 // The recurrence of one (clip, section, channel) needs 4 dependent ops per
 // frame, but sosfilt's 9 include 3 feed-forward products b_r * x that do not
-// depend on the state.  k_biquad_lane issues all 9 on the one wave whose
-// serial speed is the whole kernel's time (5/6 of the SIMDs are idle: 1024
-// clips x 5 sections x 2 channels is 171 waves).  Here a producer wave forms
+// depend on the state.  Issuing all 9 on the one wave whose serial speed is
+// the whole kernel's time (round 2's k_biquad_lane: 12.5 ms on config 4's
+// stage) leaves 5/6 of the SIMDs idle (1024 clips x 5 sections x 2 channels
+// is 171 waves).  Here a producer wave forms
 // the products one step ahead with plain v_mul_f32 (IEEE-exact, the very
 // products sosfilt takes) and hands them to the chain wave through LDS, so
 // the chain wave issues 6 VALU per frame (o = p0 + z0; t = (-a1)*o;
-// t = p1 + t; z0 = z1 + t; u = (-a2)*o; z1 = p2 + u -- bq_mf_pair's order,
-// the same ops as bq_lane_pair bit for bit).  Four waves per workgroup:
-//   chain (wave 0): lane = (clip, section, channel) as k_biquad_lane; section
+// t = p1 + t; z0 = z1 + t; u = (-a2)*o; z1 = p2 + u: sosfilt's ops bit for
+// bit, IEEE negation being exact).  Four waves per workgroup:
+//   chain (wave 0): lane = (clip, section, channel); section
 //     s filters chunk c = i - 2s - 1 at step i from its product row
 //     P[lane][(i-1) & 1] ([frame][p0 p1 p2], read by ds_read_b128) into its own
 //     planar output row O[lane][i & 1] (ds_write_b128);
@@ -657,19 +395,6 @@ constexpr size_t PC_LDS = (size_t)(PC_PL0 + 2 * PC_KPW * 2 * PC_RS) * 4;   // 15
 static_assert(PC_LDS <= 160 * 1024, "one workgroup per CU");
 static_assert(PC_PS % 64 == 4 && PC_OS % 64 == 4 && PC_RS % 64 == 4 && PC_IN0 % 4 == 0 && PC_PL0 % 4 == 0,
               "16-B rows, 4-float skew per row");
-
-#ifdef XM_BQ_PROF
-// dev: per-wave cycles of k_biquad_pc, [workgroup][wave][work, barrier wait]
-#define PC_PROF_DECL uint64_t pr_[2] = {0, 0}, tq_ = __builtin_amdgcn_s_memtime()
-#define PC_T(n) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); pr_[n] += t_ - tq_; tq_ = t_; } while (0)
-#define PC_PROF_OUT(w) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) { \
-    for (int n_ = 0; n_ < 2; ++n_) g_bq_prof[blockIdx.x * 8 + (w) * 2 + n_] = pr_[n_]; \
-    g_bq_hw[blockIdx.x * 4 + (w)] = __builtin_amdgcn_s_getreg(0xF804); } } while (0)
-#else
-#define PC_PROF_DECL do { } while (0)
-#define PC_T(n) do { } while (0)
-#define PC_PROF_OUT(w) do { } while (0)
-#endif
 
 // vmcnt(n) for a wave-uniform n <= 6 (the DMA groups of one chunk)
 __device__ __forceinline__ void pc_vm_wait(int n)
@@ -765,16 +490,12 @@ __device__ __forceinline__ void pc_load_wave(const XmhFxJob &j, int clip0, int n
     load_chunk(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     planarize(0);
-    PC_PROF_DECL;
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        PC_T(1);
         pc_vm_wait(load_chunk(i + 2));             // chunk i + 1 landed (inb[i & 1] was split at step i - 1)
         planarize(i + 1);
-        PC_T(0);
         __syncthreads();
     }
-    PC_PROF_OUT(2);
 }
 
 // The store wave: at step i the last section's output rows O[(i - 1) & 1]
@@ -808,10 +529,8 @@ __device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int 
         const int ln = ((k / CPG) * ns + ns - 1) * 4 + (k % CPG) * C;   // the chain lane of (clip, last, ch 0)
         orow[g] = PC_O0 + ln * PC_OS;
     }
-    PC_PROF_DECL;
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        PC_T(1);
         const int64_t c = i - 2 * ns;
         if (c >= 0 && c < nchunk) {
             const int p = (int)((i - 1) & 1);
@@ -837,10 +556,8 @@ __device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int 
                 }
             }
         }
-        PC_T(0);
         __syncthreads();
     }
-    PC_PROF_OUT(3);
 }
 
 template <int C, bool ST>
@@ -863,12 +580,8 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
     // the store wave (LDS reads only) as wave 2: a workgroup's waves take the
     // SIMDs in the cyclic order 0, 2, 1, 3, so wave 2 shares the chain wave's
     // half of the LDS store path, which the load wave's writes no longer
-    // contend for (7.36 -> 7.26-7.29 ms same box; dev A/B: -DXM_BQ_PC_NOSWAP)
-#ifdef XM_BQ_PC_NOSWAP
-    constexpr int W_LOAD = 2, W_STORE = 3;
-#else
+    // contend for (7.36 -> 7.26-7.29 ms same box)
     constexpr int W_LOAD = 3, W_STORE = 2;
-#endif
     if (wave == W_LOAD) {
         pc_load_wave<C>(j, clip0, nclip, steps, lf);
         return;
@@ -889,10 +602,8 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
     if (wave == 1) {
         // ---------------- producer: products one step ahead ------------------
         const int kq = valid ? kk : 0;
-        PC_PROF_DECL;
         __syncthreads();
         for (int64_t i = 0; i < steps; ++i) {
-            PC_T(1);
             const int par = (int)(i & 1);
             // chunk i - 2s: section s - 1's output row, or the planar input row
             const float *src = valid && s == 0 ? lf + PC_PL0 + ((par * PC_KPW + kq) * 2 + ch) * PC_RS
@@ -912,10 +623,8 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
                 pw[1] = f4{b1 * x[2], b2 * x[2], b1 * x[3], b2 * x[3]};
                 pw[2] = f4{b0 * x[0], b0 * x[1], b0 * x[2], b0 * x[3]};
             }
-            PC_T(0);
             __syncthreads();
         }
-        PC_PROF_OUT(1);
         return;
     }
 
@@ -927,10 +636,8 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
         z0 = st[ch];
         z1 = st[C + ch];
     }
-    PC_PROF_DECL;
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        PC_T(1);
         const int64_t c = i - 2 * s - 1;           // chunk this lane filters
         const bool act = valid && c >= 0 && c < nchunk;
         const float z0s = z0, z1s = z1;
@@ -957,7 +664,7 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
             // Per frame 4 instructions on the 4-op dependence: o = p0 + z0;
             // (t, u) = (-a1, -a2) * o (v_pk_mul_f32); (t, z1') = (p1, p2) +
             // (t, u) (v_pk_add_f32); z0 = z1 + t -- each half the very
-            // operation bq_mf_pair issues
+            // operation sosfilt takes
             const f4 *P4 = (const f4 *)Pr;
             const f2 nA = f2{na1, na2};
             f4 R[PC_CH / 4][3];
@@ -971,11 +678,11 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
 #pragma unroll
                     for (int e = 0; e < 3; ++e) R[qd + PC_RA][e] = P4[3 * (qd + PC_RA) + e];
                 }
-#ifndef XM_BQ_PC_CXX   // dev A/B: -DXM_BQ_PC_CXX, the compiler-scheduled form (7.72-7.74 ms vs 7.32-7.33 on one box)
-                // o of frames (0, 1) and (2, 3) built in place as register
-                // pairs: the product (t, u) broadcasts o from the pair's low
-                // or high half by op_sel, so no o is copied into the store
-                // pair (the compiler's form moved every odd frame's o)
+// o of frames (0, 1) and (2, 3) built in place as register pairs: the
+                // product (t, u) broadcasts o from the pair's low or high half by
+                // op_sel, so no o is copied into the store pair (the compiler-
+                // scheduled form moved every odd frame's o: 7.72-7.74 ms against
+                // 7.32-7.33 ms on one box)
                 f2 op[2];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -995,79 +702,14 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
                     z1 = r.y;
                 }
                 ((f4 *)Ow)[qd] = f4{op[0].x, op[0].y, op[1].x, op[1].y};
-#else
-                float o[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const f4 &Q = R[qd][e >> 1];
-                    const f2 p12 = (e & 1) ? f2{Q[2], Q[3]} : f2{Q[0], Q[1]};
-                    o[e] = R[qd][2][e] + z0;
-                    const f2 tu = nA * f2{o[e], o[e]};
-                    const f2 r = p12 + tu;
-                    z0 = z1 + r.x;
-                    z1 = r.y;
-                }
-                ((f4 *)Ow)[qd] = f4{o[0], o[1], o[2], o[3]};
-#endif
             }
         }
         if (!act) { z0 = z0s; z1 = z1s; }
-        PC_T(0);
         __syncthreads();                           // products of step i + 1 ready; outputs visible
     }
-    PC_PROF_OUT(0);
     if (ST && st) {
         st[ch] = z0;
         st[C + ch] = z1;
-    }
-}
-
-constexpr int FIR_THREADS = 256;
-constexpr int FIR_OPT = 4;
-constexpr int FIR_CHUNK = FIR_THREADS * FIR_OPT;
-
-template <int C>
-__global__ __launch_bounds__(FIR_THREADS) void k_fir(XmhFxJob j)
-{
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int K = j.fir_len;
-    float *h = lds;                                   // reversed taps: h[t] = fir[K-1-t]
-    float *tile = lds + ((K + 3) & ~3);
-    const int clip = blockIdx.y;
-    const float *x = j.in_ptrs[clip];
-    float *y = j.out_ptrs[clip];
-    const int64_t n0 = (int64_t)blockIdx.x * FIR_CHUNK;
-    const int64_t n1 = min(n0 + FIR_CHUNK, (int64_t)j.frames);
-    const int64_t jlo = n0 - K + 1;
-    const int span = (int)(n1 - jlo);
-    for (int i = threadIdx.x; i < K; i += FIR_THREADS) h[i] = j.fir[K - 1 - i];
-    for (int i = threadIdx.x; i < span * C; i += FIR_THREADS) {
-        const int64_t f = jlo + i / C;
-        tile[i] = f >= 0 ? x[f * C + i % C]
-                         : (j.hist_in ? j.hist_in[((int64_t)clip * (K - 1) + (K - 1 + f)) * C + i % C] : 0.0f);
-    }
-    __syncthreads();
-    float acc[FIR_OPT][C];
-#pragma unroll
-    for (int o = 0; o < FIR_OPT; ++o) {
-        const int64_t n = n0 + threadIdx.x + o * FIR_THREADS;
-#pragma unroll
-        for (int c = 0; c < C; ++c) acc[o][c] = 0.0f;
-        if (n >= n1) continue;
-        const float *xt = tile + (n - n0) * C;        // x[n-K+1] is tile[(n-n0)*C]
-        for (int t = 0; t < K; ++t) {
-            const float hv = h[t];
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc[o][c] = acc[o][c] + xt[t * C + c] * hv;
-        }
-    }
-    __syncthreads();   // in == out allowed: every read of this block's tile is done
-#pragma unroll
-    for (int o = 0; o < FIR_OPT; ++o) {
-        const int64_t n = n0 + threadIdx.x + o * FIR_THREADS;
-        if (n >= n1) continue;
-#pragma unroll
-        for (int c = 0; c < C; ++c) y[n * C + c] = acc[o][c];
     }
 }
 
@@ -1300,21 +942,9 @@ extern "C" int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream)
     if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
     if (j->n_clips == 0 || j->frames == 0) return 0;
 
-    // cascades of up to 16 sections: one recurrence per lane (k_biquad_lane);
-    // longer ones: the packed kernel.  Dev A/B builds: -DXM_BQ_PACKED_ONLY,
-    // -DXM_BQ_MF (matrix-core products: not exact, see k_biquad_lane)
-#ifdef XM_BQ_PACKED_ONLY
-    const bool mf = false;
-#else
-    const bool mf = j->n_sos <= 16;
-#endif
-#ifdef XM_BQ_MF
-    constexpr bool MFP = true;
-#else
-    constexpr bool MFP = false;
-#endif
-#ifndef XM_BQ_LANE
-    if (mf && !MFP) {   // the product path: producer / chain split (k_biquad_pc)
+    // cascades of up to 16 sections: producer / chain / load / store waves
+    // (k_biquad_pc); longer ones: the section-pipelined k_biquad_pipe
+    if (j->n_sos <= 16) {
         auto pk = j->channels == 2 ? (j->state ? k_biquad_pc<2, true> : k_biquad_pc<2, false>)
                                    : (j->state ? k_biquad_pc<1, true> : k_biquad_pc<1, false>);
         const int kpw = std::min(16 / j->n_sos * (4 / j->channels), PC_KPW);
@@ -1324,12 +954,9 @@ extern "C" int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream)
                            (hipStream_t)stream, jj);
         return hipGetLastError() == hipSuccess ? 0 : -1001;
     }
-#endif
-    auto kern = mf ? (j->channels == 2 ? (j->state ? k_biquad_lane<2, true, MFP> : k_biquad_lane<2, false, MFP>)
-                                       : (j->state ? k_biquad_lane<1, true, MFP> : k_biquad_lane<1, false, MFP>))
-                   : (j->channels == 2 ? (j->state ? k_biquad_pipe<2, true> : k_biquad_pipe<2, false>)
-                                       : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>));
-    const int kpw = mf ? std::min(16 / j->n_sos * (4 / j->channels), BQ_KPW) : std::min(64 / j->n_sos, BQ_KPW);
+    auto kern = j->channels == 2 ? (j->state ? k_biquad_pipe<2, true> : k_biquad_pipe<2, false>)
+                                 : (j->state ? k_biquad_pipe<1, true> : k_biquad_pipe<1, false>);
+    const int kpw = std::min(64 / j->n_sos, BQ_KPW);
     dim3 grid((unsigned)((j->n_clips + kpw - 1) / kpw));
     if (xmg_func_lds((const void *)kern, (int)BQ_LDS)) return -1001;   // once per (kernel, device)
     XmhFxJob jj = *j;
@@ -1337,24 +964,10 @@ extern "C" int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream)
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
 
-#ifdef XM_BQ_PROF
-extern "C" __attribute__((visibility("default"))) int xm_dev_bq_prof(uint64_t *host)
-{
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_prof), sizeof(g_bq_prof)) == hipSuccess ? 0 : -1;
-}
-extern "C" __attribute__((visibility("default"))) int xm_dev_bq_hw(uint32_t *host)
-{
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bq_hw), sizeof(g_bq_hw)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 extern "C" int xmg_launch_fx_fir(const XmhFxJob *j, void *stream)
 {
     const int K = j->fir_len;
-    const size_t lds = (size_t)(((K + 3) & ~3) + (FIR_CHUNK + K) * j->channels) * sizeof(float);
-    if (lds > 160 * 1024) return -1003;
-    dim3 grid((unsigned)((j->frames + FIR_CHUNK - 1) / FIR_CHUNK), (unsigned)j->n_clips);
-    if (grid.x == 0) return 0;
+    if (j->frames == 0 || j->n_clips == 0) return 0;
     if (j->hist_in && K > 1) {                        // streaming: next block's history first
         if (!j->hist_out || j->hist_out == j->hist_in) return -22;
         auto hk = j->channels == 1 ? k_fir_hist<1> : k_fir_hist<2>;
@@ -1362,21 +975,13 @@ extern "C" int xmg_launch_fx_fir(const XmhFxJob *j, void *stream)
                            (hipStream_t)stream, *j);
         if (hipGetLastError() != hipSuccess) return -1001;
     }
-#ifndef XM_FIR_OLD
-    {   // the register-blocked kernel (k_fir_rb)
-        const size_t rl = ((size_t)(FR_TILE + K - 1 + 14) * j->channels + 8) * sizeof(float);
-        const size_t lds_rb = std::max(rl, (size_t)FR_TILE * j->channels * sizeof(float));
-        if (lds_rb > 160 * 1024) return -1003;
-        auto kr = j->channels == 1 ? k_fir_rb<1> : k_fir_rb<2>;
-        if (lds_rb > 64 * 1024 && xmg_func_lds((const void *)kr, (int)lds_rb)) return -1001;
-        hipLaunchKernelGGL(kr, dim3((unsigned)((j->frames + FR_TILE - 1) / FR_TILE), (unsigned)j->n_clips),
-                           64 * FR_WAVES, lds_rb, (hipStream_t)stream, *j);
-        return hipGetLastError() == hipSuccess ? 0 : -1001;
-    }
-#endif
-    auto kern = j->channels == 1 ? k_fir<1> : k_fir<2>;
-    if (lds > 64 * 1024 && xmg_func_lds((const void *)kern, (int)lds)) return -1001;
-    hipLaunchKernelGGL(kern, grid, FIR_THREADS, lds, (hipStream_t)stream, *j);
+    const size_t rl = ((size_t)(FR_TILE + K - 1 + 14) * j->channels + 8) * sizeof(float);
+    const size_t lds_rb = std::max(rl, (size_t)FR_TILE * j->channels * sizeof(float));
+    if (lds_rb > 160 * 1024) return -1003;
+    auto kr = j->channels == 1 ? k_fir_rb<1> : k_fir_rb<2>;
+    if (lds_rb > 64 * 1024 && xmg_func_lds((const void *)kr, (int)lds_rb)) return -1001;
+    hipLaunchKernelGGL(kr, dim3((unsigned)((j->frames + FR_TILE - 1) / FR_TILE), (unsigned)j->n_clips),
+                       64 * FR_WAVES, lds_rb, (hipStream_t)stream, *j);
     return hipGetLastError() == hipSuccess ? 0 : -1001;
 }
 
