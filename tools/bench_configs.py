@@ -343,7 +343,7 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
     report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix"
            + (f", {ofmt} out" if oconv else ""),
            B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m, launches=launches,
-           kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
+           kernel="k_rs147_mix" if fast == launches else ("k_rs_blk / generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 
@@ -373,7 +373,7 @@ def _mono(a, name, ntr, B, fi, fo, N):
         return True
     report(name, f"{name}: {B} mixes x {ntr} mono f32 tracks x {N} frames, {fi}->{fo} f32 mix",
            B * ntr * N, B * ntr * N * 4 + B * F * 4, w, k, m, launches=launches,
-           kernel="k_rs147_mix MONO" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
+           kernel="k_rs147_mix MONO" if fast == launches else ("k_rs_blk / generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 
@@ -401,10 +401,15 @@ def c1s16(a):
         return True
     report("c1s16", f"c1s16: {B} mono s16 clips x {N} frames, 44100->48000 s16 (config 1's form)",
            B * N, B * N * 2 + B * F * 2, w, k, m, launches=launches,
-           kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
+           kernel="k_rs147_mix" if fast == launches else ("k_rs_blk / generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 
+def r32to48(a): _shape(a, "r32to48", fi=32000, fo=48000, N=320000)
+def r48to32(a): _shape(a, "r48to32", fi=48000, fo=32000, N=480000)
+def r96to44(a): _shape(a, "r96to44", fi=96000, fo=44100, N=960000, )
+def r16to48(a): _shape(a, "r16to48", fi=16000, fo=48000, N=160000)
+def m22to48(a): _mono(a, "m22to48", 1, 16 * a.mixes, 22050, 48000, 220500)
 def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)
 def mono1(a): _mono(a, "mono1", 1, 16 * a.mixes, 44100, 48000, 441000)
 def odd(a): _shape(a, "odd", N=480001)
