@@ -27,7 +27,7 @@ def _both(xm, args, kw, x, ramps=None, fx=None):
         m = xm.Mixer(*args, device=dev, **kw)
         if ramps:
             m.set_tracks(ramps)
-        if fx:
+        if fx is not None:
             e = xm.Effects(args[1], args[2], device=dev)
             for s in fx:
                 e.add_biquad(s)

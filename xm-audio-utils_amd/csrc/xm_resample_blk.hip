@@ -32,6 +32,7 @@ namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef int i4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 // the coefficient table through the constant address space: wave-uniform
 // rows are read by scalar loads into SGPRs (tap operands of the VALU ops)
 typedef const __attribute__((address_space(4))) float cfloat;
@@ -118,8 +119,11 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_blk(BlkArgs a)
                         f[2 * h + 1] = (float)(v[h] >> 16);
                     }
                 } else {
+                    // the whole vector at once (a bit_cast of one ext_vector
+                    // element lost the other elements in this compiler)
+                    const f4 vf = __builtin_bit_cast(f4, v);
 #pragma unroll
-                    for (int h = 0; h < 4; ++h) f[h] = __builtin_bit_cast(float, v[h]);
+                    for (int h = 0; h < 4; ++h) f[h] = vf[h];
                 }
 #pragma unroll
                 for (int h = 0; h < epg; ++h) {
