@@ -75,3 +75,22 @@ def test_44k_to_48k_table(header):
         assert not _bits(outside).any(), k
         assert not _bits(kHp[k // 2, pt[k // 2]:, k % 2]).any(), k
     assert sum(pt) == 1601 and pt.count(21) == 1
+
+
+@pytest.mark.parametrize("name,L,M", [("32", 3, 2), ("23", 2, 3), ("12", 1, 2)])
+def test_small_ratio_tables(header, name, L, M):
+    """The small-ratio pair tables (emit_ratio): row r = outputs (2r, 2r+1) of
+    a super-period, all T taps of both phases, rows repeating every PR pairs,
+    then one zero row."""
+    z = golden("tables.npz")
+    H, meta = z[f"H_{L}_{M}"], z[f"meta_{L}_{M}"]
+    T, rm = int(meta[2]), int(meta[3])
+    assert (int(meta[0]), int(meta[1])) == (L, M)
+    assert f"#define XM_R{name}_RM {rm}\n" in header and f"#define XM_R{name}_T {T}\n" in header
+    PR = int(re.search(rf"#define XM_R{name}_PR (\d+)", header).group(1))
+    assert PR == (L if L % 2 else L // 2)
+    kHp = _floats(_block(header, f"XM_KHP{name}_INIT", "}\n")).reshape(PR + 1, T, 2)
+    assert not _bits(kHp[PR]).any(), "the row past the last is zero"
+    for k in range(4 * L):   # two whole phase periods of outputs
+        ph = ((k + rm) * M) % L
+        assert np.array_equal(_bits(kHp[(k // 2) % PR, :, k % 2]), _bits(H[ph])), k

@@ -26,6 +26,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <algorithm>
+#include <type_traits>
 #include "xm_device.h"
 
 namespace {
@@ -53,6 +54,98 @@ struct BlkArgs {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes)
 {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// one output: r = sum over t ascending (from +0) of x[t*C + c] * h[t]; 8
+// taps per step (one scalar load of 8 coefficients, 8 LDS reads at
+// immediate offsets); stereo (L, R) in one packed pair
+template <int C>
+__device__ __forceinline__ void dot1(const float *x, cfloat *h, int T, float (&res)[2])
+{
+    int t = 0;
+    if (C == 2) {
+        const f2 *xv = (const f2 *)x;
+        f2 acc = f2{0.0f, 0.0f};
+        for (; t + 8 <= T; t += 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float ht = h[t + e];
+                acc = acc + xv[t + e] * f2{ht, ht};
+            }
+        }
+        for (; t < T; ++t) {
+            const float ht = h[t];
+            acc = acc + xv[t] * f2{ht, ht};
+        }
+        res[0] = acc.x;
+        res[1] = acc.y;
+    } else {
+        float acc = 0.0f;
+        for (; t + 8 <= T; t += 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc = acc + x[t + e] * h[t + e];
+        }
+        for (; t < T; ++t) acc = acc + x[t] * h[t];
+        res[0] = acc;
+    }
+}
+
+// two outputs whose windows start d = 0 or 1 frame apart, from one read of
+// each frame: output 0 takes x[t] * h0[t], output 1 x[t] * h1[t - d]; each
+// sum still runs over its taps in ascending order from +0
+template <int C>
+__device__ __forceinline__ void dot2(const float *x, cfloat *h0, cfloat *h1, int T, int d, float (&r0)[2],
+                                     float (&r1)[2])
+{
+    typedef typename std::conditional<C == 2, f2, float>::type V;
+    const V *xv = (const V *)x;
+    auto mul = [](V v, float hv) __attribute__((always_inline)) {
+        if constexpr (C == 2) return v * f2{hv, hv};
+        else return v * hv;
+    };
+    V a = V{}, b = V{};   // +0
+    if (d == 0) {
+        int t = 0;
+        for (; t + 8 <= T; t += 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const V v = xv[t + e];
+                a = a + mul(v, h0[t + e]);
+                b = b + mul(v, h1[t + e]);
+            }
+        }
+        for (; t < T; ++t) {
+            const V v = xv[t];
+            a = a + mul(v, h0[t]);
+            b = b + mul(v, h1[t]);
+        }
+    } else {
+        a = a + mul(xv[0], h0[0]);
+        int t = 1;
+        for (; t + 8 <= T; t += 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const V v = xv[t + e];
+                a = a + mul(v, h0[t + e]);
+                b = b + mul(v, h1[t + e - 1]);
+            }
+        }
+        for (; t < T; ++t) {
+            const V v = xv[t];
+            a = a + mul(v, h0[t]);
+            b = b + mul(v, h1[t - 1]);
+        }
+        b = b + mul(xv[T], h1[T - 1]);
+    }
+    if constexpr (C == 2) {
+        r0[0] = a.x;
+        r0[1] = a.y;
+        r1[0] = b.x;
+        r1[1] = b.y;
+    } else {
+        r0[0] = a;
+        r1[0] = b;
+    }
 }
 
 // IN16: s16 samples in memory (an s16 mix, or s16 tracks converted into an f32 one)
@@ -149,58 +242,52 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_blk(BlkArgs a)
             const int32_t gqc = xm_gain_q15(g, m_lo);
             int64_t q = qn;
             int r = rn;
-#pragma unroll
-            for (int u = 0; u < BK_KS; ++u) {
-                if (u >= ks) continue;   // wave-uniform
-                const int ph = (int)__builtin_amdgcn_readfirstlane(r);
-                const int off = (int)__builtin_amdgcn_readfirstlane((int)(q - qn));   // window offset (frames)
-                cfloat *h = (cfloat *)j.rs.H + (size_t)ph * T;
-                const float *x = row + sh + off * C;
-                float rl = 0.0f, rr = 0.0f;
-                // taps in ascending order, 8 per step (one scalar load of 8
-                // coefficients, 8 LDS reads at immediate offsets)
-                int t = 0;
-                if (C == 2) {
-                    const f2 *xv = (const f2 *)x;
-                    f2 acc = f2{0.0f, 0.0f};
-                    for (; t + 8 <= T; t += 8) {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) {
-                            const float ht = h[t + e];
-                            acc = acc + xv[t + e] * f2{ht, ht};
-                        }
-                    }
-                    for (; t < T; ++t) {
-                        const float ht = h[t];
-                        acc = acc + xv[t] * f2{ht, ht};
-                    }
-                    rl = acc.x;
-                    rr = acc.y;
-                } else {
-                    float acc = 0.0f;
-                    for (; t + 8 <= T; t += 8) {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) acc = acc + x[t + e] * h[t + e];
-                    }
-                    for (; t < T; ++t) acc = acc + x[t] * h[t];
-                    rl = acc;
-                }
-                const int64_t m = ob + i_lane + k0 + u;          // absolute output frame of this lane
-                if (S16) {
-                    const int32_t gq = gconst ? gqc : xm_gain_q15(g, m);
-                    acci[u][0] += xm_q15_term(xm_round_sat16(rl), gq);
-                    if (C == 2) acci[u][C - 1] += xm_q15_term(xm_round_sat16(rr), gq);
-                } else {
-                    const float gf = gconst ? gfc : xm_gain_f32(g, m);
-                    accf[u][0] = accf[u][0] + gf * rl;
-                    if (C == 2) accf[u][C - 1] = accf[u][C - 1] + gf * rr;
-                }
+            auto step = [&]() __attribute__((always_inline)) {   // to the next output
                 r += a.dr;
                 q += a.dq;
                 if (r >= L) {
                     r -= L;
                     ++q;
                 }
+            };
+            auto take = [&](int u, const float (&v)[2]) __attribute__((always_inline)) {   // gain, ordered sum
+                const int64_t m = ob + i_lane + k0 + u;          // absolute output frame of this lane
+                if (S16) {
+                    const int32_t gq = gconst ? gqc : xm_gain_q15(g, m);
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acci[u][c] += xm_q15_term(xm_round_sat16(v[c]), gq);
+                } else {
+                    const float gf = gconst ? gfc : xm_gain_f32(g, m);
+#pragma unroll
+                    for (int c = 0; c < C; ++c) accf[u][c] = accf[u][c] + gf * v[c];
+                }
+            };
+            // outputs in pairs: when the second window starts 0 or 1 frame
+            // after the first (every upsampling ratio; most frames of mild
+            // downsampling) one LDS read per tap feeds both
+#pragma unroll
+            for (int u = 0; u < BK_KS; u += 2) {
+                if (u >= ks) continue;   // wave-uniform
+                const bool two = u + 1 < ks;
+                const int ph0 = (int)__builtin_amdgcn_readfirstlane(r);
+                const int off0 = (int)__builtin_amdgcn_readfirstlane((int)(q - qn));   // window offset (frames)
+                step();
+                const int ph1 = (int)__builtin_amdgcn_readfirstlane(r);
+                const int off1 = (int)__builtin_amdgcn_readfirstlane((int)(q - qn));
+                step();
+                cfloat *h0 = (cfloat *)j.rs.H + (size_t)ph0 * T;
+                cfloat *h1 = (cfloat *)j.rs.H + (size_t)ph1 * T;
+                const float *x0 = row + sh + off0 * C;
+                float v0[2] = {0.0f, 0.0f}, v1[2] = {0.0f, 0.0f};
+                const int d = off1 - off0;
+                if (two && (d == 0 || d == 1)) {
+                    dot2<C>(x0, h0, h1, T, d, v0, v1);
+                } else {
+                    dot1<C>(x0, h0, T, v0);
+                    if (two) dot1<C>(row + sh + off1 * C, h1, T, v1);
+                }
+                take(u, v0);
+                if (two) take(u + 1, v1);
             }
         }
         // ---- store the lane's ks outputs

@@ -9,7 +9,8 @@
  * coefficient inline (no scalar loads).  Tap 22 of every phase must be an exact
  * zero (the 160-frame pre-pad); the generator refuses otherwise.
  *
- * and the 44.1k->48k tables (emit_up).
+ * and the 44.1k->48k tables (emit_up), and the small-ratio pair tables
+ * (emit_ratio: 3/2, 2/3, 1/2, 2/1).
  *
  * usage: gen_coefs <out.h>
  */
@@ -77,6 +78,43 @@ static int emit_up(FILE *f)
     return 0;
 }
 
+/* The small-L/M ratios of the fused kernel (RatioBase<RID> in
+ * csrc/xm_resample_fast.hip): every output runs all T taps, and the phase of
+ * output k, ((k + rm) * M) % L, repeats every L outputs, so the pair rows
+ * (outputs 2i, 2i+1) repeat every PR = L / gcd(L, 2) pairs.  Emits
+ *     XM_R<name>_RM, XM_R<name>_T, XM_R<name>_PR and
+ *     XM_KHP<name>_INIT[PR + 1][2T]: row i = (h_2i[t], h_2i+1[t]) for t < T,
+ * plus one zero row (the last coefficient group of a row reads up to 16
+ * floats past its start).  The design depends on L and M only. */
+static int emit_ratio(FILE *f, const char *name, int L, int M)
+{
+    XmResampleDesign d;
+    if (xm_resample_design(M, L, &d, NULL) || d.L != L || d.M != M) return 1;
+    float *H = calloc((size_t)(L * d.T), sizeof(float));
+    if (!H || xm_resample_design(M, L, &d, H)) {
+        free(H);
+        return 1;
+    }
+    const int PR = L % 2 ? L : L / 2;
+    fprintf(f, "// %d/%d (xm_resample_design(%d, %d)): T = %d, rm = %d, pair rows repeat every %d\n", L, M, M, L, d.T,
+            d.rm, PR);
+    fprintf(f, "#define XM_R%s_RM %d\n#define XM_R%s_T %d\n#define XM_R%s_PR %d\n", name, d.rm, name, d.T, name, PR);
+    fprintf(f, "#define XM_KHP%s_INIT { \\\n", name);
+    for (int i = 0; i <= PR; ++i) {
+        fprintf(f, "  {");
+        for (int t = 0; t < d.T; ++t)
+            for (int j = 0; j < 2; ++j) {
+                const int k = 2 * i + j;
+                const float v = i < PR ? H[(((k + d.rm) * M) % L) * d.T + t] : 0.0f;
+                fprintf(f, "%s%af", t || j ? ", " : "", (double)v);
+            }
+        fprintf(f, "}, \\\n");
+    }
+    fprintf(f, "}\n");
+    free(H);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc != 2) {
@@ -125,5 +163,8 @@ int main(int argc, char **argv)
         fprintf(f, "}, \\\n");
     }
     fprintf(f, "}\n");
-    return emit_up(f) || fclose(f) ? 1 : 0;
+    return emit_up(f) || emit_ratio(f, "32", 3, 2) || emit_ratio(f, "23", 2, 3) || emit_ratio(f, "12", 1, 2) ||
+                   emit_ratio(f, "21", 2, 1) || fclose(f)
+               ? 1
+               : 0;
 }

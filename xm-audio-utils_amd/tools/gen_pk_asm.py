@@ -136,7 +136,9 @@ for n in range(1, 5):
     for first in (True, False):
         for two in (True, False):
             out.append(f'#define XM_V2_{"F" if first else "R"}{n}_{"TWO" if two else "ONE"} "{vblock(n, first, two)}"')
-for first, n, name in ((True, 8, "G0"), (False, 8, "G1"), (False, 6, "G2"), (False, 5, "G2T5"), (False, 4, "G2T4")):
+# G2T<n>: an n-tap last group (1..7 taps: every ratio's T mod 8)
+for first, n, name in ((True, 8, "G0"), (False, 8, "G1"), (False, 6, "G2")) + tuple(
+        (False, n, f"G2T{n}") for n in (1, 2, 3, 4, 5, 7)):
     for two in (True, False):
         out.append(f'#define XM_PK_{name}_{"TWO" if two else "ONE"} "{block(n, first, two)}"')
 for n in (2, 4):
