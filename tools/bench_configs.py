@@ -379,7 +379,8 @@ def _mono(a, name, ntr, B, fi, fo, N):
 
 def c1s16(a):
     """Config 1's own form (mono s16 44.1k -> 48k, unity Q15 gain), batched:
-    8192 clips through Mixer(44100, 48000, 1, "s16"), the generic kernel."""
+    8192 clips through Mixer(44100, 48000, 1, "s16"): the fused kernel's mono
+    s16 (M16) 1-track rows."""
     B, N = 16 * a.mixes, 441000
     m = xm.Mixer(44100, 48000, 1, "s16", mem="device")
     ramps = [dict(gain0_q15=32768)]
