@@ -1,15 +1,15 @@
 #!/bin/bash
 # GPU pass (from the repo root via gpurun): GPU tests, smoke, the driver's
 # bench line, the one-process sharded bench forms, config 5, the loud
-# failure of --gpus N beyond the visible devices, and optionally config lines
-# and fused-kernel ablations (lib_ablate).  Each GPU step has its own time
+# failure of --gpus N beyond the visible devices, and optionally config
+# lines.  Each GPU step has its own time
 # limit; the script stops at the first failure.
-#   tools/gpu_pass.sh <tag> [--no-tests] [--no-bench] [--configs "c2 c3 ..."] [--ablate "base abl1 ..."]
+#   tools/gpu_pass.sh <tag> [--no-tests] [--no-bench] [--configs "c2 c3 ..."]
 set -o pipefail
 TAG=${1:-r3}; shift
-TESTS=1; BENCH=1; CFGS=""; ABL=""
+TESTS=1; BENCH=1; CFGS=""
 while [ $# -gt 0 ]; do
-  case $1 in --no-tests) TESTS=0 ;; --no-bench) BENCH=0 ;; --configs) CFGS=$2; shift ;; --ablate) ABL=$2; shift ;; esac
+  case $1 in --no-tests) TESTS=0 ;; --no-bench) BENCH=0 ;; --configs) CFGS=$2; shift ;; esac
   shift
 done
 OUT=gpurun_out/$TAG
@@ -40,8 +40,5 @@ if [ $BENCH = 1 ]; then
 fi
 if [ -n "$CFGS" ]; then
   step configs 900 python3 -u tools/bench_configs.py $CFGS
-fi
-if [ -n "$ABL" ]; then
-  step ablate 900 python3 -u tools/ablate.py $ABL
 fi
 echo "gpu_pass done: $OUT"

@@ -3,7 +3,7 @@
 # from the repo root).  One --pmc pass per counter set, never combined with
 # tracing; each pass under its own time limit; stop at the first failure.
 #   tools/pmc_fast.sh <tag> [bench args...]
-# Extra environment (e.g. XM_AUDIO_LIB / XM_FAST_ABLATE) passes through.
+# Extra environment (e.g. XM_AUDIO_LIB) passes through.
 TAG=${1:-pmc}; shift
 ARGS=${@:---steps 3 --warmup 1 --no-cpu}
 OUT=gpurun_out/pmc_$TAG
