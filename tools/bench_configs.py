@@ -343,7 +343,7 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
     report(name, f"{name}: {B} mixes x {ntr} stereo {ifmt} tracks x {N} frames, {fi}->{fo} {fmt} mix"
            + (f", {ofmt} out" if oconv else ""),
            B * ntr * N * 2, B * ntr * N * 2 * isz + B * F * 2 * osz, w, k, m, launches=launches,
-           kernel="k_rs147_mix" if fast == launches else ("k_rs_blk / generic" if not fast else f"{fast}/{launches} fused"),
+           kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 
@@ -373,7 +373,7 @@ def _mono(a, name, ntr, B, fi, fo, N):
         return True
     report(name, f"{name}: {B} mixes x {ntr} mono f32 tracks x {N} frames, {fi}->{fo} f32 mix",
            B * ntr * N, B * ntr * N * 4 + B * F * 4, w, k, m, launches=launches,
-           kernel="k_rs147_mix MONO" if fast == launches else ("k_rs_blk / generic" if not fast else f"{fast}/{launches} fused"),
+           kernel="k_rs147_mix MONO" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 
@@ -402,7 +402,7 @@ def c1s16(a):
         return True
     report("c1s16", f"c1s16: {B} mono s16 clips x {N} frames, 44100->48000 s16 (config 1's form)",
            B * N, B * N * 2 + B * F * 2, w, k, m, launches=launches,
-           kernel="k_rs147_mix" if fast == launches else ("k_rs_blk / generic" if not fast else f"{fast}/{launches} fused"),
+           kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
 
 

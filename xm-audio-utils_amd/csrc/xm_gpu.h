@@ -21,7 +21,6 @@ int xmg_func_lds(const void *kern, int bytes);
 
 int xmg_launch_mix_fast(const XmhMixJob *j, void *stream, int *n_launches);      /* xm_resample_fast.hip */
 int xmg_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_launches);   /* xm_mix_generic.hip */
-int xmg_launch_resample_blk(const XmhMixJob *j, void *stream, int *n_launches);  /* xm_resample_blk.hip */
 int xmg_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches);
 int xmg_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
                           int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream);
