@@ -39,8 +39,9 @@ Also reported (one JSON line on rank 0):
                  written once) / average kernel duration from HIP events on
                  the stream the kernel runs on, vs the 8 TB/s HBM peak;
                  traffic: corrected PMC bytes per launch from the newest
-                 profiles/*traffic*.json (an earlier rocprofv3 pass; the
-                 file is named in traffic_source).
+                 profiles/*traffic*.json taken on the same kernel sources
+                 (sha256 of KERNEL_SOURCES; an earlier rocprofv3 pass, the
+                 file named in traffic_source), else null.
   cpu_baseline — the library's own host CPU backend (n_devices = 0,
                  xm-audio-utils_amd/src/cpu: the same C API call, bit-identical
                  results) on a bounded sample of the same workload, in a child
@@ -150,18 +151,44 @@ def plan(args, world: int, visible: int):
     return "local", devs
 
 
+# the sources the headline kernel is compiled from: a PMC traffic record
+# counts for this run only if it was taken on these very sources
+KERNEL_SOURCES = ("xm-audio-utils_amd/csrc/xm_resample_fast.hip", "xm-audio-utils_amd/csrc/xm_pk_taps.h",
+                  "xm-audio-utils_amd/csrc/xm_device.h", "xm-audio-utils_amd/csrc/xm_shim.h",
+                  "xm-audio-utils_amd/tools/gen_coefs.c")
+
+
+def kernel_src_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def traffic_from_profiles():
-    """Latest corrected PMC traffic per launch (tools/profile_traffic.py output)
-    and the file it came from (a separate rocprofv3 pass, not this run)."""
+    """Corrected PMC traffic per launch (tools/profile_traffic.py output) from
+    the newest profiles/*traffic*.json taken on this tree's kernel sources
+    (its kernel_src_sha256 equals ours), and the file it came from (a separate
+    rocprofv3 pass, not this run).  None when no record matches: a number
+    measured on other kernel code is not reported as this kernel's traffic."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
     if not files:
         return None, None
     try:
-        with open(files[-1]) as fh:
-            d = json.load(fh)
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
-    except (OSError, ValueError):
+        mine = kernel_src_sha256()
+    except OSError:
         return None, None
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel_src_sha256") == mine:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+    return None, f"none on these kernel sources (newest record: {os.path.relpath(files[-1], ROOT)})"
 
 
 def cpu_model():

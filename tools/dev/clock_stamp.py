@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--fill", choices=["synth", "zero"], default="synth")
     ap.add_argument("--label", default="")
+    ap.add_argument("--span", type=int, default=0, help="also time N single launches: first start to last end")
     args = ap.parse_args()
     fn = getattr(xm._lib, "xm_dev_clock", None)
     if fn is None:
@@ -67,8 +68,21 @@ def main():
         for _ in range(20):
             step()
         torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 4)()
-    fn(buf)   # clear
+    buf = (C.c_ulonglong * 8)()
+    fn(buf)   # clear (the first read also resets the min slots)
+    fn(buf)
+    if args.span:   # single launches: dispatch ramp and tail per launch
+        ramp, tail, span = [], [], []
+        for _ in range(args.span):
+            step()
+            torch.cuda.synchronize()
+            fn(buf)
+            ramp.append((buf[5] - buf[4]) / 100.0)       # us: last wave start - first wave start
+            tail.append((buf[3] - buf[6]) / 100.0)       # us: last wave end - first wave end
+            span.append((buf[3] - buf[4]) / 100.0)       # us: first start to last end
+        print(json.dumps({"label": args.label, "mixes": B, "launches": args.span,
+                          "span_us": sorted(span)[len(span) // 2], "dispatch_ramp_us": sorted(ramp)[len(ramp) // 2],
+                          "end_spread_us": sorted(tail)[len(tail) // 2]}), flush=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()

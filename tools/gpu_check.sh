@@ -26,6 +26,7 @@ step() {   # step <name> <seconds> <cmd...>
 }
 rocminfo 2>/dev/null | grep -m3 -E 'gfx950|Compute Unit' > $OUT/rocminfo.txt || true
 nproc > $OUT/nproc.txt
+python3 -c "import bench; print(bench.kernel_src_sha256())" > $OUT/kernel_src.sha256
 if [ $TESTS = 1 ]; then
   step pytest_gpu 600 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"

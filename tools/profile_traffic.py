@@ -11,7 +11,8 @@ from the separate FETCH_SIZE and WRITE_SIZE passes, corrected as
   * on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
     streaming read (16 B/lane global_load and buffer_load ... lds alike), so
     it is doubled; WRITE_SIZE is exact for streaming stores.
-bench.py reads the newest profiles/*traffic*.json for roofline.traffic.
+bench.py reads the newest profiles/*traffic*.json taken on its own kernel
+sources (kernel_src_sha256, written by tools/gpu_check.sh) for roofline.traffic.
 """
 import csv
 import json
@@ -61,6 +62,10 @@ def main():
         "rocprof_avg_ms": avg_ns / 1e6 if avg_ns else None,
         "rocprof_achieved_GBps": (ALG_READ + ALG_WRITE) / avg_ns if avg_ns else None,
     }
+    # the kernel sources the pass ran (bench.py reports this record only for them)
+    sha = os.path.join(src, "kernel_src.sha256")
+    if os.path.exists(sha):
+        rec["kernel_src_sha256"] = open(sha).read().strip()
     with open(dst + "_traffic.json", "w") as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec, indent=1))
