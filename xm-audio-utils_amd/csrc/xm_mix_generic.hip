@@ -73,6 +73,24 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
     for (int o = 0; o < GEN_OPT; ++o)
 #pragma unroll
         for (int c = 0; c < C; ++c) { accf[o][c] = 0.0f; acci[o][c] = 0; }
+    // phase and window start of each of the thread's outputs, once for all
+    // tracks: (m + rm) * M = (m0 + rm) * M + d * M with d < GEN_CHUNK, so one
+    // 64-bit division per thread and 32-bit ones per output (d * M + r0 <
+    // 2^23 for M <= 4096)
+    int hoff[GEN_OPT], xoff[GEN_OPT];
+    {
+        const int64_t Mx0 = (m0 + rm) * M;
+        const int64_t q0 = Mx0 / L;
+        const int r0 = (int)(Mx0 - q0 * L);
+        const int qb = (int)(q0 - T + 1 - jlo);
+#pragma unroll
+        for (int o = 0; o < GEN_OPT; ++o) {
+            const int u = r0 + (int)(threadIdx.x + o * GEN_THREADS) * M;
+            const int qu = u / L;
+            hoff[o] = (u - qu * L) * T;          // phase row of H
+            xoff[o] = (qb + qu) * C;             // window start in the tile
+        }
+    }
 
     for (int tr = 0; tr < j.n_tracks; ++tr) {
         __syncthreads();
@@ -98,15 +116,16 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
         }
         __syncthreads();
         const XmhGain g = j.gains[tr];
+        // a gain constant over the block's outputs: evaluated once per track
+        const bool gconst = xm_gain_const(g, m0, m1 - 1);
+        const float gfc = S16 ? 0.0f : xm_gain_f32(g, m0);
+        const int32_t gqc = S16 ? xm_gain_q15(g, m0) : 0;
 #pragma unroll
         for (int o = 0; o < GEN_OPT; ++o) {
             const int64_t m = m0 + threadIdx.x + o * GEN_THREADS;
             if (m >= m1) continue;
-            const int64_t Mx = (m + rm) * M;
-            const int ph = (int)(Mx % L);
-            const int jb = (int)(Mx / L - T + 1 - jlo);
-            const float *h = H + ph * T;
-            const float *xt = tile + jb * C;
+            const float *h = H + hoff[o];
+            const float *xt = tile + xoff[o];
             float r[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) r[c] = 0.0f;
@@ -116,11 +135,11 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
                 for (int c = 0; c < C; ++c) r[c] = r[c] + xt[t * C + c] * hv;
             }
             if (S16) {
-                const int32_t gq = xm_gain_q15(g, m);
+                const int32_t gq = gconst ? gqc : xm_gain_q15(g, m);
 #pragma unroll
                 for (int c = 0; c < C; ++c) acci[o][c] += xm_q15_term(xm_round_sat16(r[c]), gq);
             } else {
-                const float gf = xm_gain_f32(g, m);
+                const float gf = gconst ? gfc : xm_gain_f32(g, m);
 #pragma unroll
                 for (int c = 0; c < C; ++c) accf[o][c] = accf[o][c] + gf * r[c];
             }
