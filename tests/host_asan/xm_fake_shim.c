@@ -429,6 +429,13 @@ static int fk_reduce_scatter_i32(const int32_t *send, int32_t *recv, size_t recv
 
 static int fk_comm_check(void *comm) { return comm ? 0 : -1002; }
 
+static int fk_stream_wait(void *s, void *e)   /* fake launches complete in their call */
+{
+    (void)s;
+    (void)e;
+    return 0;
+}
+
 const XmhBackend xmh_gpu = {
     "fake-gfx950",
     fk_device_count, fk_set_device, fk_malloc, fk_free, fk_host_alloc, fk_host_free,
@@ -436,5 +443,5 @@ const XmhBackend xmh_gpu = {
     fk_memset, fk_memcpy2d, fk_event_create, fk_event_destroy, fk_event_record, fk_event_elapsed,
     fk_pointer_is_device, fk_memcpy_peer, fk_comm_init_all, fk_comm_destroy, fk_group_start, fk_group_end,
     fk_reduce_scatter_i32, fk_comm_check, fk_arch_name, fk_launch_mix, fk_launch_mix_window, fk_launch_fx,
-    fk_launch_mix_placed, fk_launch_finish_s16, fk_fast_table_check, fk_synth,
+    fk_launch_mix_placed, fk_launch_finish_s16, fk_fast_table_check, fk_synth, fk_stream_wait,
 };

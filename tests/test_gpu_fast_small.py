@@ -1,6 +1,7 @@
 """The fused kernel at the small-L/M ratios (SURVEY.md
 §8(a) a1-a2): 3/2 (32k -> 48k, 16k -> 24k), 2/3 (48k -> 32k) and 1/2
-(96k -> 48k), stereo f32 interleaved tracks, 1-8 tracks per mix.  A
+(96k -> 48k): stereo f32 interleaved tracks, mono f32 tracks and mono s16
+tracks into the Q15 mix, 1-8 tracks per mix.  A
 super-period is P periods (160 or 159 input frames) and every output runs all
 T taps of its phase (RatioBase<RID_32/23/12> in csrc/xm_resample_fast.hip).
 Every case must run on the fused kernel (XmMixerTiming.fast_launches == 1)
@@ -169,3 +170,50 @@ def test_small_production_grid_32_48(xm, gpu):
     assert not bool(y.isnan().any())
     del x, y
     torch.cuda.empty_cache()
+
+
+def _xm1(B, nt, N, base, s16=False):
+    g = O.gen_s16 if s16 else O.gen_f32
+    return np.stack([np.stack([g(SEED, base + 16 * b + t, 1, N) for t in range(nt)]) for b in range(B)])
+
+
+@pytest.mark.parametrize("ratio", RATIOS, ids=IDS)
+@pytest.mark.parametrize("nt", [1, 3, 8])
+def test_small_mono_f32(xm, gpu, ratio, nt):
+    """Mono f32 tracks at the small ratios (the MONO instantiations: a lane's
+    run in two halves riding as the planar pair), odd and even N."""
+    fi, fo, L, M, SPI = ratio
+    for N in (20 * SPI + 37, 20 * SPI + 38, 2 * SPI - 1):
+        B = 11 if nt == 1 else 3
+        x = _xm1(B, nt, N, 25000 + N + nt)
+        ramps = _ramps(nt, _F(N, L, M))
+        m = xm.Mixer(fi, fo, 1, "f32")
+        m.set_tracks(ramps)
+        y = m.process(x)
+        t = m.timing()
+        # 3/2 one-track mono rows: the generic kernel (vmcnt bound, see xmg_fast_kern_mono_r32)
+        assert t.n_launches == 1 and t.fast_launches == (0 if (L, M, nt) == (3, 2, 1) else 1)
+        ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)
+        assert bits_equal(y, ref), N
+
+
+@pytest.mark.parametrize("ratio", RATIOS, ids=IDS)
+@pytest.mark.parametrize("nt", [1, 5])
+def test_small_mono_s16_q15(xm, gpu, ratio, nt):
+    """Mono s16 tracks into the Q15 mix at the small ratios (M16; 2/3 moves
+    every other SP origin by one s16 frame), dword-aligned N on the fused
+    kernel, odd N on the generic one."""
+    fi, fo, L, M, SPI = ratio
+    for N in (20 * SPI + 38, 2 * SPI + 2, 20 * SPI + 37):
+        B = 11 if nt == 1 else 3
+        x = _xm1(B, nt, N, 26000 + N + nt, s16=True)
+        F = _F(N, L, M)
+        q = [dict(gain0_q15=32768 - 3000 * t, gain1_q15=1000 * t, ramp_start=37 * t, ramp_len=max(1, F // 3)) for t in range(nt)]
+        m = xm.Mixer(fi, fo, 1, "s16")
+        m.set_tracks(q)
+        y = m.process(x)
+        t = m.timing()
+        fused = N % 2 == 0 and (L, M, nt) != (3, 2, 1)
+        assert t.n_launches == 1 and t.fast_launches == (1 if fused else 0), (N, t.fast_launches)
+        ref = np.stack([CO.resample_mix_s16(list(x[b]), q, L, M) for b in range(B)])
+        assert bits_equal(y, ref), N

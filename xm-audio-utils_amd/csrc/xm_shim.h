@@ -147,6 +147,8 @@ int  xmh_event_create(void **e);
 void xmh_event_destroy(void *e);
 int  xmh_event_record(void *e, void *s);
 int  xmh_event_elapsed(float *ms, void *e0, void *e1);  /* syncs e1 */
+/* work enqueued on s after this call waits for the last record of e */
+int  xmh_stream_wait(void *s, void *e);
 int  xmh_pointer_is_device(const void *p);     /* 1 device, 0 host, <0 error */
 /* device-to-device copy between (possibly different) devices, on stream s */
 int  xmh_memcpy_peer(void *dst, int dst_dev, const void *src, int src_dev, size_t bytes, void *s);
@@ -229,6 +231,7 @@ typedef struct XmhBackend {
     int (*fast_table_check)(const float *H, int L, int M, int T);
     int (*synth)(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips, int channels, int64_t frames,
                  void *stream);
+    int (*stream_wait)(void *s, void *e);
 } XmhBackend;
 extern const XmhBackend xmh_gpu;   /* csrc/xm_shim.hip (tests/host_asan: a CPU stand-in) */
 extern const XmhBackend xmh_cpu;   /* src/cpu/xm_cpu_backend.c */

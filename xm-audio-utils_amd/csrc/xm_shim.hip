@@ -178,6 +178,7 @@ void xmg_event_destroy(void *e)
 }
 
 int xmg_event_record(void *e, void *s) { return map(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); }
+int xmg_stream_wait(void *s, void *e) { return map(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0)); }
 
 int xmg_event_elapsed(float *ms, void *e0, void *e1)
 {
@@ -372,7 +373,7 @@ const XmhBackend xmh_gpu = {
     xmg_memset, xmg_memcpy2d, xmg_event_create, xmg_event_destroy, xmg_event_record, xmg_event_elapsed,
     xmg_pointer_is_device, xmg_memcpy_peer, xmg_comm_init_all, xmg_comm_destroy, xmg_group_start, xmg_group_end,
     xmg_reduce_scatter_i32, xmg_comm_check, xmg_arch_name, xmg_launch_mix, xmg_launch_mix_window, xmg_launch_fx,
-    xmg_launch_mix_placed, xmg_launch_finish_s16, xmg_fast_table_check, xmg_synth,
+    xmg_launch_mix_placed, xmg_launch_finish_s16, xmg_fast_table_check, xmg_synth, xmg_stream_wait,
 };
 #endif
 

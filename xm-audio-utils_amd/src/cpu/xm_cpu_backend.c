@@ -205,6 +205,14 @@ int xmc_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips
     return xmc_parallel(n_clips, item_synth, &s);
 }
 
+/* every CPU job completes inside its call: nothing to wait for */
+static int c_stream_wait(void *s, void *e)
+{
+    (void)s;
+    (void)e;
+    return 0;
+}
+
 const XmhBackend xmh_cpu = {
     "cpu",
     c_device_count, c_set_device, c_malloc, c_free, c_malloc, c_free,
@@ -212,5 +220,5 @@ const XmhBackend xmh_cpu = {
     c_memset, c_memcpy2d, c_event_create, c_event_destroy, c_event_record, c_event_elapsed,
     c_pointer_is_device, c_memcpy_peer, c_comm_init_all, c_comm_destroy, c_group, c_group,
     c_reduce_scatter_i32, c_comm_check, c_arch_name, xmc_launch_mix, c_launch_mix_window, xmc_launch_fx,
-    xmc_launch_mix_placed, xmc_launch_finish_s16, c_fast_table_check, xmc_synth,
+    xmc_launch_mix_placed, xmc_launch_finish_s16, c_fast_table_check, xmc_synth, c_stream_wait,
 };

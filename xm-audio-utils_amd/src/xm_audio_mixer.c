@@ -15,6 +15,8 @@
 
 #include "xm_internal.h"
 
+#define XM_FX_BLOCKS 8   /* time blocks of the config-4 pipeline */
+
 struct XmAudioMixer {
     XmMixerConfig cfg;
     int n_tracks;
@@ -52,6 +54,15 @@ struct XmAudioMixer {
     int64_t *place_dev;            /* [XM_MAX_TRACKS][2] */
     XmhGain *unity_dev;            /* one unity-gain descriptor */
     XmMulti *multi;                /* multi-device handle: every call dispatches here */
+    /* the time-block pipeline of resample -> biquad cascades -> mix (config 4,
+     * run_fx_pipelined): two internal streams, events per block, the biquad
+     * states and the per-block pointer tables */
+    void *fx_s[2];
+    void *fx_ev[3][XM_FX_BLOCKS];
+    float *fx_state;
+    size_t fx_state_cap;
+    void **fx_dtab, **fx_htab;
+    size_t fx_tab_cap;
 };
 
 void *xm_mixer_stream(const XmAudioMixer *m) { return m->stream; }
@@ -222,6 +233,16 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
     xmh_free(m->unity_dev);
     xmh_free(m->d_ptrs);
     xmh_host_free(m->h_ptrs);
+    for (int i = 0; i < 2; ++i)
+        if (m->fx_s[i]) {
+            xmh_stream_sync(m->fx_s[i]);
+            xmh_stream_destroy(m->fx_s[i]);
+        }
+    for (int a = 0; a < 3; ++a)
+        for (int k = 0; k < XM_FX_BLOCKS; ++k) xmh_event_destroy(m->fx_ev[a][k]);
+    xmh_free(m->fx_state);
+    xmh_free(m->fx_dtab);
+    xmh_host_free(m->fx_htab);
     for (int i = 0; i < 6; ++i) xmh_event_destroy(m->ev[i]);
     xmh_stream_destroy(m->own_stream);
     free(m);
@@ -411,6 +432,156 @@ static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *
 /* Effects path (config 4): resample every track into scratch at unity gain,
  * run the chain on each track in place, then the no-resample mix with the
  * track gains.  Order per track: resample -> effects -> gain -> ordered sum. */
+/* Config 4 as a time-block pipeline.  The biquad stage is
+ * serial in time and its chain waves hold only a few SIMDs, so the output is
+ * cut into XM_FX_BLOCKS blocks of whole 147-output super-periods: block k is
+ * resampled on the caller's stream, filtered on fx_s[0] (section states carry
+ * from block to block, as in xm_effects_process_stream) once its resample has
+ * landed, and mixed on fx_s[1] once filtered.  The resample of block k + 1 and
+ * the mix of block k - 1 run beside the biquad of block k.  Every output is
+ * the same kernel arithmetic as the three whole-clip passes (window jobs of
+ * the same kernels, absolute gain indices), so the result is bit-identical.
+ * XM_ENOSYS: not this path's shape (the caller runs the three passes). */
+static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStage *st, int ns, float *scratch,
+                            int *launches)
+{
+    const int C = j0->channels, ntr = j0->n_tracks;
+    const int64_t F = j0->frames_out, N = j0->frames_in;
+    const size_t ntot = (size_t)j0->n_mix * (size_t)ntr;
+    const size_t per_track = (size_t)F * (size_t)C;
+    if (m->cfg.device == XMH_DEV_CPU || ns < 1 || j0->in_ptrs || j0->out_ptrs || j0->io_flags || j0->in_base ||
+        j0->out_base || j0->window || F < 64 * 147 * XM_FX_BLOCKS)
+        return XM_ENOSYS;
+    if (j0->n_mix > 1 && j0->in_mix_stride != (int64_t)ntr * j0->in_track_stride) return XM_ENOSYS;
+    int max_sos = 0;
+    for (int s = 0; s < ns; ++s) {
+        if (st[s].kind != 1) return XM_ENOSYS;   /* FIR stages: history handling, the three passes */
+        max_sos = st[s].n > max_sos ? st[s].n : max_sos;
+    }
+    const int64_t L = m->table.d.L, M = m->table.d.M;
+    const int fused = L == 147 && M == 160 && m->table.fast;   /* window jobs of the fused kernel */
+    int64_t Fb = (F + XM_FX_BLOCKS - 1) / XM_FX_BLOCKS;
+    Fb = (Fb + 146) / 147 * 147;                               /* whole super-periods */
+    const int K = (int)((F + Fb - 1) / Fb);
+    int rc = XM_OK;
+    for (int i = 0; !rc && i < 2; ++i)
+        if (!m->fx_s[i]) rc = xmh_stream_create(&m->fx_s[i]);
+    for (int a = 0; !rc && a < 3; ++a)
+        for (int k = 0; !rc && k < XM_FX_BLOCKS; ++k)
+            if (!m->fx_ev[a][k]) rc = xmh_event_create(&m->fx_ev[a][k]);
+    if (!rc && !m->unity_dev) {
+        static const XmhGain ug = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
+        rc = xmh_malloc((void **)&m->unity_dev, sizeof ug);
+        if (!rc) rc = xmh_memcpy_h2d(m->unity_dev, &ug, sizeof ug, m->stream);
+    }
+    /* biquad states [stage][clip][section][z0, z1][channel], zero at clip start */
+    const size_t st_floats = (size_t)ns * ntot * (size_t)max_sos * 2u * (size_t)C;
+    if (!rc && m->fx_state_cap < st_floats) {
+        xmh_free(m->fx_state);
+        m->fx_state = NULL;
+        m->fx_state_cap = 0;
+        rc = xmh_malloc((void **)&m->fx_state, st_floats * sizeof(float));
+        if (!rc) m->fx_state_cap = st_floats;
+    }
+    /* block k's track pointers (scratch rows from the block's first frame) */
+    const size_t ntab = (size_t)K * ntot;
+    if (!rc && m->fx_tab_cap < ntab) {
+        xmh_free(m->fx_dtab);
+        xmh_host_free(m->fx_htab);
+        m->fx_dtab = m->fx_htab = NULL;
+        m->fx_tab_cap = 0;
+        rc = xmh_malloc((void **)&m->fx_dtab, ntab * sizeof(void *));
+        if (!rc) rc = xmh_host_alloc((void **)&m->fx_htab, ntab * sizeof(void *));
+        if (!rc) m->fx_tab_cap = ntab;
+    }
+    if (rc) return rc;
+    for (int k = 0; k < K; ++k)
+        for (size_t i = 0; i < ntot; ++i) m->fx_htab[(size_t)k * ntot + i] = scratch + i * per_track + (size_t)k * Fb * C;
+    void *sb = m->fx_s[0], *sm = m->fx_s[1];
+    /* the biquad stream starts after everything earlier on the caller's stream */
+    rc = xmh_event_record(m->fx_ev[2][0], m->stream);
+    if (!rc) rc = xmh_stream_wait(sb, m->fx_ev[2][0]);
+    if (!rc) rc = xmh_stream_wait(sm, m->fx_ev[2][0]);
+    if (!rc) rc = xmh_memcpy_h2d(m->fx_dtab, m->fx_htab, ntab * sizeof(void *), sb);
+    if (!rc) rc = xmh_memset(m->fx_state, 0, st_floats * sizeof(float), sb);
+    static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
+    const int64_t elem = (int64_t)in_bytes(m);
+    for (int k = 0; !rc && k < K; ++k) {
+        const int64_t o0 = (int64_t)k * Fb, bl = (F - o0) < Fb ? (F - o0) : Fb;
+        /* 1) resample block k of every track (1-track unity mixes) */
+        XmhMixJob r = *j0;
+        r.n_tracks = 1;
+        r.n_mix = (int32_t)ntot;
+        r.in_mix_stride = j0->in_track_stride;   /* track i of the flat list */
+        r.in_track_stride = 0;
+        r.gains = m->unity_dev;
+        r.gains_host = &unity_gain;
+        r.unity = 1;
+        r.out_conv = 0;
+        r.out = scratch + (size_t)o0 * C;
+        r.out_mix_stride = (int64_t)per_track;
+        r.frames_out = bl;
+        rc = XM_ENOSYS;
+        if (fused) {   /* window: input from the block's super-period origin, the 32 frames before it real */
+            const int64_t a0 = o0 / 147 * 160;
+            XmhMixJob w = r;
+            w.in = (const char *)j0->in + a0 * C * elem;
+            w.frames_in = N - a0;
+            w.window = a0 > 0;
+            rc = xmh_launch_mix_window(&w, m->stream, launches, &m->timing.fast_launches);
+        }
+        if (rc == XM_ENOSYS) {   /* any kernel: absolute output window */
+            r.out_base = o0;
+            rc = xmh_launch_mix(&r, m->stream, launches, &m->timing.fast_launches);
+        }
+        if (!rc) rc = xmh_event_record(m->fx_ev[0][k], m->stream);
+        /* 2) the biquad cascades on block k, states carried */
+        if (!rc) rc = xmh_stream_wait(sb, m->fx_ev[0][k]);
+        for (int s = 0; !rc && s < ns; ++s) {
+            XmhFxJob fj;
+            memset(&fj, 0, sizeof fj);
+            fj.channels = C;
+            fj.n_clips = (int32_t)ntot;
+            fj.frames = bl;
+            fj.in_ptrs = (const float *const *)(m->fx_dtab + (size_t)k * ntot);
+            fj.out_ptrs = (float *const *)(m->fx_dtab + (size_t)k * ntot);
+            fj.sos = st[s].coef_dev;
+            fj.n_sos = st[s].n;
+            fj.state = m->fx_state + (size_t)s * ntot * (size_t)max_sos * 2u * (size_t)C;
+            rc = xmh_launch_fx(&fj, sb, launches);
+        }
+        if (!rc) rc = xmh_event_record(m->fx_ev[1][k], sb);
+        /* 3) the gained, ordered mix of block k */
+        if (!rc) rc = xmh_stream_wait(sm, m->fx_ev[1][k]);
+        if (!rc) {
+            XmhMixJob x = *j0;
+            x.in = scratch + (size_t)o0 * C;
+            x.in_ptrs = NULL;
+            x.in_ptrs_host = NULL;
+            x.in_track_stride = (int64_t)per_track;
+            x.in_mix_stride = (int64_t)(per_track * (size_t)ntr);
+            x.frames_in = bl;
+            x.frames_out = bl;
+            x.out_base = o0;
+            x.out = (char *)j0->out + (size_t)o0 * C * (size_t)out_bytes(m);
+            x.rs.L = x.rs.M = 1;
+            x.rs.T = 1;
+            x.rs.rm = 0;
+            x.unity = 0;
+            x.rs.fast = 0;
+            rc = xmh_launch_mix(&x, sm, launches, &m->timing.fast_launches);
+        }
+    }
+    /* the caller's stream continues after the last mix */
+    if (!rc) rc = xmh_event_record(m->fx_ev[2][1], sm);
+    if (!rc) rc = xmh_stream_wait(m->stream, m->fx_ev[2][1]);
+    if (rc) {   /* leave nothing in flight on the internal streams */
+        xmh_stream_sync(sb);
+        xmh_stream_sync(sm);
+    }
+    return rc;
+}
+
 static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
 {
     const int C = j0->channels, ntr = j0->n_tracks;
@@ -428,6 +599,11 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     if (rc) return rc;
     float *scratch = (float *)m->d_fx;
     float *scratch2 = (float *)((char *)m->d_fx + buf_bytes);
+    rc = run_fx_pipelined(m, j0, st, ns, scratch, launches);
+    if (rc != XM_ENOSYS) {
+        if (!rc) rc = xmh_stream_sync(m->stream);
+        return rc;
+    }
     /* 1) resample: treat every track as its own 1-track mix (unity gain) */
     static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
     XmhGain *ug = NULL;
