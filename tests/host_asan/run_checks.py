@@ -169,6 +169,20 @@ def main():
     rf = np.stack([CO.mix_f32([CO.fir_f32(CO.biquad_f32(CO.resample_f32(x[b, t], 147, 160), sos), h)
                                for t in range(8)], RAMPS) for b in range(2)])
     check("mixer with per-track effects", beq(yf, rf))
+    # config 4's time-block pipeline (biquad-only chains, >= 64 super-periods
+    # per block): resample, biquad with carried states and mix per block on
+    # three streams; the stand-in runs the generic window jobs
+    eb = xm.Effects(44100, 2)
+    for sv in sos:
+        eb.add_biquad(sv)
+    mp = xm.Mixer(48000, 44100, 2, "f32")
+    mp.set_tracks(RAMPS)
+    mp.set_track_effects(eb)
+    xp = f32_tracks(2, 8, 82000, base=90)
+    yp = mp.process(xp)
+    rp = np.stack([CO.mix_f32([CO.biquad_f32(CO.resample_f32(xp[b, t], 147, 160), sos) for t in range(8)], RAMPS)
+                   for b in range(2)])
+    check("config-4 time-block pipeline", beq(yp, rp) and mp.timing().n_launches >= 3 * 8)
 
     # multi-device handles (XM_FAKE_DEVICES=2): distinct devices and a repeated one
     for devs in ([0, 1], [0, 0, 1]):

@@ -562,7 +562,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
             x.in_mix_stride = (int64_t)(per_track * (size_t)ntr);
             x.frames_in = bl;
             x.frames_out = bl;
-            x.out_base = o0;
+            x.in_base = x.out_base = o0;   /* row 0 of the block is absolute frame o0 (gains at absolute frames) */
             x.out = (char *)j0->out + (size_t)o0 * C * (size_t)out_bytes(m);
             x.rs.L = x.rs.M = 1;
             x.rs.T = 1;
