@@ -77,7 +77,7 @@ def test_44k_to_48k_table(header):
     assert sum(pt) == 1601 and pt.count(21) == 1
 
 
-@pytest.mark.parametrize("name,L,M", [("32", 3, 2), ("23", 2, 3), ("12", 1, 2)])
+@pytest.mark.parametrize("name,L,M", [("32", 3, 2), ("23", 2, 3), ("12", 1, 2), ("21", 2, 1), ("31", 3, 1)])
 def test_small_ratio_tables(header, name, L, M):
     """The small-ratio pair tables (emit_ratio): row r = outputs (2r, 2r+1) of
     a super-period, all T taps of both phases, rows repeating every PR pairs,

@@ -217,3 +217,27 @@ def test_small_mono_s16_q15(xm, gpu, ratio, nt):
         assert t.n_launches == 1 and t.fast_launches == (1 if fused else 0), (N, t.fast_launches)
         ref = np.stack([CO.resample_mix_s16(list(x[b]), q, L, M) for b in range(B)])
         assert bits_equal(y, ref), N
+
+
+# 2/1 and 3/1: 320 and 480 outputs per super-period, 8-track rows only
+UPRATIOS = [(24000, 48000, 2, 1, 160), (16000, 48000, 3, 1, 160)]
+
+
+@pytest.mark.parametrize("ratio", UPRATIOS, ids=["2_1", "3_1"])
+@pytest.mark.parametrize("nt", [1, 2, 5, 8])
+def test_up_small_mixes(xm, gpu, ratio, nt):
+    """Stereo f32 mixes at 2/1 (24k -> 48k) and 3/1 (16k -> 48k) on the fused
+    kernel (2-8 tracks; 1-track resample-only batches take the generic
+    kernel), odd and even N, lengths around super-period edges."""
+    fi, fo, L, M, SPI = ratio
+    for N in (20 * SPI + 37, 20 * SPI + 38, SPI - 1, SPI + 1, 2 * SPI + 1, 7):
+        B = 3
+        x = _x(B, nt, N, 27000 + N + nt)
+        ramps = _ramps(nt, _F(N, L, M))
+        m = xm.Mixer(fi, fo, 2, "f32")
+        m.set_tracks(ramps)
+        y = m.process(x)
+        t = m.timing()
+        assert t.n_launches == 1 and t.fast_launches == (1 if nt >= 2 else 0), (N, t.fast_launches)
+        ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)
+        assert bits_equal(y, ref), N

@@ -410,6 +410,7 @@ def r32to48(a): _shape(a, "r32to48", fi=32000, fo=48000, N=320000)
 def r48to32(a): _shape(a, "r48to32", fi=48000, fo=32000, N=480000)
 def r96to44(a): _shape(a, "r96to44", fi=96000, fo=44100, N=960000, )
 def r96to48(a): _shape(a, "r96to48", fi=96000, fo=48000, N=960000)
+def r24to48(a): _shape(a, "r24to48", fi=24000, fo=48000, N=240000)
 def r16to48(a): _shape(a, "r16to48", fi=16000, fo=48000, N=160000)
 def m22to48(a): _mono(a, "m22to48", 1, 16 * a.mixes, 22050, 48000, 220500)
 def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)

@@ -10,7 +10,7 @@
  * zero (the 160-frame pre-pad); the generator refuses otherwise.
  *
  * and the 44.1k->48k tables (emit_up), and the small-ratio pair tables
- * (emit_ratio: 3/2, 2/3, 1/2, 2/1).
+ * (emit_ratio: 3/2, 2/3, 1/2, 2/1, 3/1).
  *
  * usage: gen_coefs <out.h>
  */
@@ -164,7 +164,7 @@ int main(int argc, char **argv)
     }
     fprintf(f, "}\n");
     return emit_up(f) || emit_ratio(f, "32", 3, 2) || emit_ratio(f, "23", 2, 3) || emit_ratio(f, "12", 1, 2) ||
-                   emit_ratio(f, "21", 2, 1) || fclose(f)
+                   emit_ratio(f, "21", 2, 1) || emit_ratio(f, "31", 3, 1) || fclose(f)
                ? 1
                : 0;
 }
