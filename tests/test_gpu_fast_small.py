@@ -241,3 +241,30 @@ def test_up_small_mixes(xm, gpu, ratio, nt):
         assert t.n_launches == 1 and t.fast_launches == (1 if nt >= 2 else 0), (N, t.fast_launches)
         ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)
         assert bits_equal(y, ref), N
+
+
+@pytest.mark.parametrize("ratio", RATIOS, ids=IDS)
+@pytest.mark.parametrize("nt", [4, 8])
+def test_small_stereo_s16(xm, gpu, ratio, nt):
+    """Stereo s16 tracks at the small ratios (the IO instantiations, 8-track
+    rows): the s16 Q15 mix and s16 tracks into the f32 mix, odd and even N."""
+    fi, fo, L, M, SPI = ratio
+    for N in (20 * SPI + 37, 20 * SPI + 38, SPI + 1):
+        B = 3
+        xs = np.stack([np.stack([O.gen_s16(SEED, 28000 + N + 16 * b + t, 2, N) for t in range(nt)]) for b in range(B)])
+        F = _F(N, L, M)
+        q = [dict(gain0_q15=29491 - 1000 * t, gain1_q15=3000 * t, ramp_start=200 * t, ramp_len=max(1, F // 4))
+             for t in range(nt)]
+        m = xm.Mixer(fi, fo, 2, "s16")
+        m.set_tracks(q)
+        y = m.process(xs)
+        _fast(m)
+        for b in range(B):
+            assert bits_equal(y[b], CO.resample_mix_s16(list(xs[b]), q, L, M)), (N, b)
+        ramps = _ramps(nt, F)
+        c = xm.Mixer(fi, fo, 2, "f32", convert_in=True)
+        c.set_tracks(ramps)
+        yc = c.process(xs)
+        _fast(c)
+        xf = xs.astype(np.float32) * np.float32(2.0 ** -15)
+        assert bits_equal(yc, CO.batch_resample_mix_f32(xf, ramps, L, M, threads=4)[0]), N
