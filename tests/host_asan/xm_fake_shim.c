@@ -436,6 +436,13 @@ static int fk_stream_wait(void *s, void *e)   /* fake launches complete in their
     return 0;
 }
 
+/* as if 256 CUs: the partitioned pipeline runs here too */
+static int fk_stream_create_cus(void **s, int lo, int hi, int *n_cus)
+{
+    *n_cus = 8 * (hi - lo);
+    return s ? fk_stream_create(s) : 0;
+}
+
 const XmhBackend xmh_gpu = {
     "fake-gfx950",
     fk_device_count, fk_set_device, fk_malloc, fk_free, fk_host_alloc, fk_host_free,
@@ -444,4 +451,5 @@ const XmhBackend xmh_gpu = {
     fk_pointer_is_device, fk_memcpy_peer, fk_comm_init_all, fk_comm_destroy, fk_group_start, fk_group_end,
     fk_reduce_scatter_i32, fk_comm_check, fk_arch_name, fk_launch_mix, fk_launch_mix_window, fk_launch_fx,
     fk_launch_mix_placed, fk_launch_finish_s16, fk_fast_table_check, fk_synth, fk_stream_wait,
+    fk_stream_create_cus,
 };

@@ -243,6 +243,59 @@ def test_up_small_mixes(xm, gpu, ratio, nt):
         assert bits_equal(y, ref), N
 
 
+@pytest.mark.parametrize("ratio", RATIOS + UPRATIOS, ids=IDS + ["2_1", "3_1"])
+@pytest.mark.parametrize("nt", [2, 8])
+def test_small_multi_sp_runs(xm, gpu, ratio, nt):
+    """Batches large enough that each lane walks several super-periods (R >= 2:
+    the carry, the previous SP's last round stored in the next SP, the next
+    SP's segment 2 loaded during this one).  Every output of every mix is
+    checked; the small-batch tests above run one SP per lane.  (At 2/1 and 3/1
+    the next SP's segment-2 DMA once ran past its 8 parts into the exchange
+    rows: wrong last rounds at the production bench shape.)"""
+    import torch
+    fi, fo, L, M, SPI = ratio
+    B, N = (64, 48000) if nt == 2 else (48, 96000)   # B * N / 160 SPs > 16384: R >= 2
+    x = _x(B, nt, N, 29000 + nt)
+    ramps = _ramps(nt, _F(N, L, M))
+    m = xm.Mixer(fi, fo, 2, "f32", mem="device")
+    m.set_tracks(ramps)
+    F = m.out_frames(N)
+    xd = torch.from_numpy(x).cuda()
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    m.process_strided(xd.data_ptr(), N * 2, N * 2 * nt, y.data_ptr(), F * 2, B, N)
+    torch.cuda.synchronize()
+    _fast(m)
+    ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=8)
+    assert bits_equal(y.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("ratio", UPRATIOS, ids=["2_1", "3_1"])
+def test_up_small_production_grid(xm, gpu, ratio):
+    """The 24k -> 48k and 16k -> 48k bench lines' shape (512 mixes x 8 tracks x
+    10 s): first and last mixes bit-checked, nothing left unwritten."""
+    import torch
+    fi, fo, L, M, SPI = ratio
+    B, nt, N = 512, 8, fi * 10
+    ramps = _ramps(nt, _F(N, L, M))
+    m = xm.Mixer(fi, fo, 2, "f32", mem="device")
+    m.set_tracks(ramps)
+    F = m.out_frames(N)
+    x = torch.empty((B * nt, N, 2), dtype=torch.float32, device="cuda")
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    xm.synth(x.data_ptr(), "f32", SEED, 0, B * nt, 2, N)
+    torch.cuda.synchronize()
+    m.process_strided(x.data_ptr(), N * 2, N * 2 * nt, y.data_ptr(), F * 2, B, N)
+    torch.cuda.synchronize()
+    _fast(m)
+    for b in (0, B - 1):
+        xb = x[b * nt:(b + 1) * nt].cpu().numpy()[None]
+        ref, _ = CO.batch_resample_mix_f32(xb, ramps, L, M, threads=8)
+        assert bits_equal(y[b].cpu().numpy(), ref[0]), b
+    assert not bool(y.isnan().any())
+    del x, y
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("ratio", RATIOS, ids=IDS)
 @pytest.mark.parametrize("nt", [4, 8])
 def test_small_stereo_s16(xm, gpu, ratio, nt):

@@ -353,50 +353,52 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
     }
 }
 
-// ---- producer / chain split: k_biquad_pc ------------------------------------
+// ---- chain / load / store split: k_biquad_pc -------------------------------
 // The recurrence of one (clip, section, channel) needs 4 dependent ops per
-// frame, but sosfilt's 9 include 3 feed-forward products b_r * x that do not
-// depend on the state.  Issuing all 9 on the one wave whose serial speed is
-// the whole kernel's time (round 2's k_biquad_lane: 12.5 ms on config 4's
-// stage) leaves 5/6 of the SIMDs idle (1024 clips x 5 sections x 2 channels
-// is 171 waves).  Here a producer wave forms
-// the products one step ahead with plain v_mul_f32 (IEEE-exact, the very
-// products sosfilt takes) and hands them to the chain wave through LDS, so
-// the chain wave issues 6 VALU per frame (o = p0 + z0; t = (-a1)*o;
-// t = p1 + t; z0 = z1 + t; u = (-a2)*o; z1 = p2 + u: sosfilt's ops bit for
-// bit, IEEE negation being exact).  Four waves per workgroup:
-//   chain (wave 0): lane = (clip, section, channel); section
-//     s filters chunk c = i - 2s - 1 at step i from its product row
-//     P[lane][(i-1) & 1] ([frame][p0 p1 p2], read by ds_read_b128) into its own
-//     planar output row O[lane][i & 1] (ds_write_b128);
-//   producer (wave 1): lane (clip, s, ch) forms the products of chunk i - 2s
-//     into P[lane][i & 1] from section s-1's output row O[lane-4][(i-1) & 1]
-//     (section 0: the planar input row PL[i & 1][clip][ch]), 16-B reads all;
-//   load (wave 2): the DMA of chunk i + 2 (global_load_lds_dwordx4 by per-lane
+// frame; sosfilt's other ops are the 3 feed-forward products b_r * x, which do
+// not depend on the state.  Lane = (clip, section, channel): the sections of a
+// cascade are a pipeline across lanes, section s filtering chunk i - s at
+// step i from section s-1's output row of step i - 1 (section 0: the planar
+// input row).  The chain lane forms the products itself (v_mul_f32 /
+// v_pk_mul_f32, IEEE-exact: the very products sosfilt takes) in the issue
+// slots the dependent chain leaves idle, so per frame it issues 6 VALU (p0 =
+// b0*x; (p1, p2) = (b1, b2)*x; o = p0 + z0; (t, u) = (-a1, -a2)*o; (t, z1') =
+// (p1, p2) + (t, u); z0 = z1 + t: sosfilt's ops bit for bit, IEEE negation
+// being exact) and moves 2 floats through LDS (its source frame in, its
+// output out).  Round 3 handed the products from a producer wave through LDS
+// (3 floats written and 3 read per frame, 13 of the workgroup's LDS floats per
+// lane-frame against 4 here): the chain ran 39 cycles per frame, LDS-bound,
+// against 24.4 for the bare recurrence (tools/ubench/bq_pk_chain.hip).
+// Waves per workgroup:
+//   chain (wave 0): section s filters chunk c = i - s from its source row
+//     (16 ds_read_b128, the whole 64-frame chunk read first) into its own
+//     planar output row O[lane][i & 1] (ds_write_b128 per 4 frames);
+//   load (wave 3): the DMA of chunk i + 2 (global_load_lds_dwordx4 by per-lane
 //     64-bit addresses, 4 / C clips per instruction) into inb[i & 1], waiting
 //     only for chunk i + 1, which it then splits into the planar rows
 //     PL[(i + 1) & 1] -- every chunk has two steps to land;
-//   store (wave 3): the last section's rows O[(i - 1) & 1] (chunk i - 2 ns),
-//     interleaved in registers, to HBM, never waiting for a store.
+//   store (wave 2): the last section's rows O[(i - 1) & 1] (chunk i - ns),
+//     interleaved in registers, to HBM, never waiting for a store;
+//   wave 1 only keeps the barrier count (the SIMD order 0, 2, 1, 3 puts the
+//     store wave beside the chain wave on the LDS store path).
 // One barrier per step; chunks are 64 frames.  Rows are skewed by 4 floats
 // per row so the 16-B row accesses of a wave are bank-conflict free.
 constexpr int PC_CH = 64;                          // frames per chunk (per channel)
 constexpr int PC_KPW = 12;                         // clips per workgroup at most
-#ifndef PC_RA
-#define PC_RA 6                                    // chain: product quads read ahead
-#endif
-constexpr int PC_PS = 2 * PC_CH * 3 + 4;           // floats per lane: P[parity][frame][3] + skew
 constexpr int PC_OS = 2 * PC_CH + 4;               // floats per lane: O[parity][frame] + skew
 constexpr int PC_RS = PC_CH + 4;                   // floats per planar input row + skew
-constexpr int PC_O0 = 64 * PC_PS;                  // O rows (floats); P rows start at 0
+constexpr int PC_O0 = 0;                           // O rows (floats)
 constexpr int PC_IN0 = PC_O0 + 64 * PC_OS;         // inb[chunk & 1][clip]: chunks of PC_CH * C floats, contiguous
 constexpr int PC_PL0 = PC_IN0 + 2 * PC_KPW * PC_CH * 2;   // PL[chunk & 1][clip][ch]: rows of PC_RS floats
-constexpr size_t PC_LDS = (size_t)(PC_PL0 + 2 * PC_KPW * 2 * PC_RS) * 4;   // 158,464 B
-static_assert(PC_LDS <= 160 * 1024, "one workgroup per CU");
-static_assert(PC_PS % 64 == 4 && PC_OS % 64 == 4 && PC_RS % 64 == 4 && PC_IN0 % 4 == 0 && PC_PL0 % 4 == 0,
+constexpr size_t PC_LDS = (size_t)(PC_PL0 + 2 * PC_KPW * 2 * PC_RS) * 4;   // 59,136 B
+// two workgroups per CU (src/xm_audio_mixer.c run_fx_pipelined sizes its CU
+// partition for that; 128-frame chunks, 116 KB: bq 7.07 ms against 7.36, but
+// one workgroup per CU)
+static_assert(PC_LDS <= 80 * 1024, "two workgroups per CU");
+static_assert(PC_OS % 64 == 4 && PC_RS % 64 == 4 && PC_IN0 % 4 == 0 && PC_PL0 % 4 == 0,
               "16-B rows, 4-float skew per row");
 
-// vmcnt(n) for a wave-uniform n <= 6 (the DMA groups of one chunk)
+// vmcnt(n) for a wave-uniform n <= 12 (the DMA groups of one chunk)
 __device__ __forceinline__ void pc_vm_wait(int n)
 {
     switch (n) {
@@ -406,6 +408,12 @@ __device__ __forceinline__ void pc_vm_wait(int n)
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
@@ -424,7 +432,7 @@ __device__ __forceinline__ void pc_load_wave(const XmhFxJob &j, int clip0, int n
     constexpr int LPC = CB / 16;                   // lanes per clip chunk
     constexpr int CPI = 64 / LPC;                  // clips per DMA instruction
     constexpr int NG = PC_KPW / CPI;               // instruction groups at most
-    static_assert(NG <= 6, "pc_vm_wait covers 6 groups");
+    static_assert(NG <= 12, "pc_vm_wait covers 12 groups");
     const int lane = threadIdx.x & 63;
     const int64_t N = j.frames;
     const int64_t nchunk = (N + PC_CH - 1) / PC_CH, nfull = N / PC_CH;
@@ -499,7 +507,7 @@ __device__ __forceinline__ void pc_load_wave(const XmhFxJob &j, int clip0, int n
 }
 
 // The store wave: at step i the last section's output rows O[(i - 1) & 1]
-// (chunk i - 2 ns) -> interleaved 16-B segments -> HBM; it never waits for a
+// (chunk i - ns) -> interleaved 16-B segments -> HBM; it never waits for a
 // store.
 template <int C>
 __device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, int ns,
@@ -531,7 +539,7 @@ __device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int 
     }
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        const int64_t c = i - 2 * ns;
+        const int64_t c = i - ns;
         if (c >= 0 && c < nchunk) {
             const int p = (int)((i - 1) & 1);
 #pragma unroll
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
     const int nclip = min(kpw, j.n_clips - clip0);
     const int64_t N = j.frames;
     const int64_t nchunk = (N + PC_CH - 1) / PC_CH;
-    const int64_t steps = nchunk + 2 * ns + 1;
+    const int64_t steps = nchunk + ns + 1;
     const int wave = threadIdx.x >> 6;
     // the store wave (LDS reads only) as wave 2: a workgroup's waves take the
     // SIMDs in the cyclic order 0, 2, 1, 3, so wave 2 shares the chain wave's
@@ -590,46 +598,24 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
         pc_store_wave<C>(j, clip0, nclip, steps, ns, lf);
         return;
     }
+    if (wave == 1) {   // barriers only
+        __syncthreads();
+        for (int64_t i = 0; i < steps; ++i) __syncthreads();
+        return;
+    }
     const int lane = threadIdx.x & 63;
     const int blk = lane >> 2, r = lane & 3;
     const int grp = blk / ns, s = blk % ns, ci = r / C, ch = r % C;
     const int kk = grp * CPG + ci;
     const bool valid = blk < gpw * ns && kk < nclip;
+    const int kq = valid ? kk : 0;
     const float *q = j.sos + 6 * (valid ? s : 0);
     const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
-    const int P_lane = lane * PC_PS, O_lane = PC_O0 + lane * PC_OS;
-
-    if (wave == 1) {
-        // ---------------- producer: products one step ahead ------------------
-        const int kq = valid ? kk : 0;
-        __syncthreads();
-        for (int64_t i = 0; i < steps; ++i) {
-            const int par = (int)(i & 1);
-            // chunk i - 2s: section s - 1's output row, or the planar input row
-            const float *src = valid && s == 0 ? lf + PC_PL0 + ((par * PC_KPW + kq) * 2 + ch) * PC_RS
-                                               : lf + (valid ? O_lane - 4 * PC_OS : O_lane) + (par ^ 1) * PC_CH;
-            float *Pw = lf + P_lane + par * PC_CH * 3;
-            // the whole source row first: the compiler cannot move these reads
-            // past the product writes (same LDS array), and one read per quad
-            // would expose the LDS latency 16 times a step
-            f4 xr[PC_CH / 4];
-#pragma unroll
-            for (int qd = 0; qd < PC_CH / 4; ++qd) xr[qd] = ((const f4 *)src)[qd];
-#pragma unroll
-            for (int qd = 0; qd < PC_CH / 4; ++qd) {
-                const f4 x = xr[qd];
-                f4 *pw = (f4 *)(Pw + 12 * qd);
-                pw[0] = f4{b1 * x[0], b2 * x[0], b1 * x[1], b2 * x[1]};
-                pw[1] = f4{b1 * x[2], b2 * x[2], b1 * x[3], b2 * x[3]};
-                pw[2] = f4{b0 * x[0], b0 * x[1], b0 * x[2], b0 * x[3]};
-            }
-            __syncthreads();
-        }
-        return;
-    }
+    const int O_lane = PC_O0 + lane * PC_OS;
 
     // ---------------- chain: 6 VALU per frame ---------------------------------
     const float na1 = -a1, na2 = -a2;              // (-a)*o == -(a*o): IEEE negation is exact
+    const f2 nA = f2{na1, na2}, B12 = f2{b1, b2};
     float z0 = 0.0f, z1 = 0.0f;
     float *st = (ST && valid) ? j.state + ((size_t)(clip0 + kk) * ns + s) * 2 * C : nullptr;
     if (ST && st) {
@@ -638,19 +624,28 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
     }
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
-        const int64_t c = i - 2 * s - 1;           // chunk this lane filters
+        const int64_t c = i - s;                   // chunk this lane filters
         const bool act = valid && c >= 0 && c < nchunk;
         const float z0s = z0, z1s = z1;
         const int par = (int)(i & 1);
-        const float *Pr = lf + P_lane + (par ^ 1) * PC_CH * 3;
+        // chunk c: section s-1's output row (written at step i - 1), or the
+        // planar input row (chunk i, split by the load wave at step i - 1)
+        const float *src = valid && s == 0 ? lf + PC_PL0 + ((par * PC_KPW + kq) * 2 + ch) * PC_RS
+                                           : lf + (valid ? O_lane - 4 * PC_OS : O_lane) + (par ^ 1) * PC_CH;
         float *Ow = lf + O_lane + par * PC_CH;
+        // the whole source chunk first (the compiler cannot move these reads
+        // past the output writes: same LDS array)
+        f4 X[PC_CH / 4];
+#pragma unroll
+        for (int qd = 0; qd < PC_CH / 4; ++qd) X[qd] = ((const f4 *)src)[qd];
         const bool tail = ST && st && act && (c + 1) * PC_CH > N;
         if (__builtin_amdgcn_ballot_w64(tail) != 0) {
             // a streamed block's last chunk: frames past N are padding and must
             // not advance the state (wave-uniform branch)
+#pragma unroll
             for (int f = 0; f < PC_CH; ++f) {
-                const float *q = Pr + 12 * (f >> 2);
-                const float p0 = q[8 + (f & 3)], p1 = q[2 * (f & 3)], p2 = q[2 * (f & 3) + 1];
+                const float x = X[f >> 2][f & 3];
+                const float p0 = b0 * x, p1 = b1 * x, p2 = b2 * x;
                 const float o = p0 + z0;
                 if (!(tail && c * PC_CH + f >= N)) {
                     z0 = z1 + (p1 + na1 * o);
@@ -659,26 +654,13 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
                 Ow[f] = o;
             }
         } else {
-            // quads of 4 frames (12 products = 3 x 16 B: (p1, p2) of frames
-            // 0-1, of frames 2-3, p0 of frames 0-3), read PC_RA quads ahead.
-            // Per frame 4 instructions on the 4-op dependence: o = p0 + z0;
-            // (t, u) = (-a1, -a2) * o (v_pk_mul_f32); (t, z1') = (p1, p2) +
-            // (t, u) (v_pk_add_f32); z0 = z1 + t -- each half the very
-            // operation sosfilt takes
-            const f4 *P4 = (const f4 *)Pr;
-            const f2 nA = f2{na1, na2};
-            f4 R[PC_CH / 4][3];
-#pragma unroll
-            for (int qd = 0; qd < PC_RA; ++qd)
-#pragma unroll
-                for (int e = 0; e < 3; ++e) R[qd][e] = P4[3 * qd + e];
+            // quads of 4 frames.  Per frame 4 instructions on the 4-op
+            // dependence: o = p0 + z0; (t, u) = (-a1, -a2) * o (v_pk_mul_f32);
+            // (t, z1') = (p1, p2) + (t, u) (v_pk_add_f32); z0 = z1 + t -- each
+            // half the very operation sosfilt takes; the products off it
 #pragma unroll
             for (int qd = 0; qd < PC_CH / 4; ++qd) {
-                if (qd + PC_RA < PC_CH / 4) {
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) R[qd + PC_RA][e] = P4[3 * (qd + PC_RA) + e];
-                }
-// o of frames (0, 1) and (2, 3) built in place as register pairs: the
+                // o of frames (0, 1) and (2, 3) built in place as register pairs: the
                 // product (t, u) broadcasts o from the pair's low or high half by
                 // op_sel, so no o is copied into the store pair (the compiler-
                 // scheduled form moved every odd frame's o: 7.72-7.74 ms against
@@ -686,26 +668,27 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
                 f2 op[2];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const f4 &Q = R[qd][e >> 1];
-                    const f2 p12 = (e & 1) ? f2{Q[2], Q[3]} : f2{Q[0], Q[1]};
+                    const float x = X[qd][e];
+                    const float p0 = b0 * x;
+                    const f2 p12 = B12 * f2{x, x};
                     f2 &oo = op[e >> 1];
                     f2 tu;
                     if (e & 1) {
-                        oo.y = R[qd][2][e] + z0;
+                        oo.y = p0 + z0;
                         asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(tu) : "v"(nA), "v"(oo));
                     } else {
-                        oo.x = R[qd][2][e] + z0;
+                        oo.x = p0 + z0;
                         asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(tu) : "v"(nA), "v"(oo));
                     }
-                    const f2 r = p12 + tu;
-                    z0 = z1 + r.x;
-                    z1 = r.y;
+                    const f2 rr = p12 + tu;
+                    z0 = z1 + rr.x;
+                    z1 = rr.y;
                 }
                 ((f4 *)Ow)[qd] = f4{op[0].x, op[0].y, op[1].x, op[1].y};
             }
         }
         if (!act) { z0 = z0s; z1 = z1s; }
-        __syncthreads();                           // products of step i + 1 ready; outputs visible
+        __syncthreads();                           // chunk i + 1's source rows ready; outputs visible
     }
     if (ST && st) {
         st[ch] = z0;

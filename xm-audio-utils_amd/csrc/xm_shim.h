@@ -149,6 +149,11 @@ int  xmh_event_record(void *e, void *s);
 int  xmh_event_elapsed(float *ms, void *e0, void *e1);  /* syncs e1 */
 /* work enqueued on s after this call waits for the last record of e */
 int  xmh_stream_wait(void *s, void *e);
+/* a stream whose kernels run only on the CUs i with lo <= i % 32 < hi (a
+ * partition even across the 8 XCDs for lo, hi multiples of 8); *n_cus = how
+ * many CUs that is (0: no CU masks on this backend, a plain stream).  s NULL:
+ * only the count */
+int  xmh_stream_create_cus(void **s, int lo, int hi, int *n_cus);
 int  xmh_pointer_is_device(const void *p);     /* 1 device, 0 host, <0 error */
 /* device-to-device copy between (possibly different) devices, on stream s */
 int  xmh_memcpy_peer(void *dst, int dst_dev, const void *src, int src_dev, size_t bytes, void *s);
@@ -232,6 +237,7 @@ typedef struct XmhBackend {
     int (*synth)(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips, int channels, int64_t frames,
                  void *stream);
     int (*stream_wait)(void *s, void *e);
+    int (*stream_create_cus)(void **s, int lo, int hi, int *n_cus);
 } XmhBackend;
 extern const XmhBackend xmh_gpu;   /* csrc/xm_shim.hip (tests/host_asan: a CPU stand-in) */
 extern const XmhBackend xmh_cpu;   /* src/cpu/xm_cpu_backend.c */

@@ -180,6 +180,29 @@ void xmg_event_destroy(void *e)
 int xmg_event_record(void *e, void *s) { return map(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); }
 int xmg_stream_wait(void *s, void *e) { return map(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0)); }
 
+// CU-masked stream (config 4's pipeline: the biquad workgroups each need a
+// whole CU's LDS, so the stages beside them keep to the other CUs)
+int xmg_stream_create_cus(void **s, int lo, int hi, int *n_cus)
+{
+    const int cus = xmg_cu_count();
+    uint32_t mask[64] = {};
+    const int words = (cus + 31) / 32;
+    int n = 0;
+    for (int i = 0; i < cus && i < 64 * 32; ++i)
+        if (i % 32 >= lo && i % 32 < hi) {
+            mask[i / 32] |= 1u << (i % 32);
+            ++n;
+        }
+    *n_cus = n;
+    if (!s) return 0;
+    *s = nullptr;
+    if (n == 0 || words > 64) return -22;
+    hipStream_t h = nullptr;
+    const int rc = map(hipExtStreamCreateWithCUMask(&h, (uint32_t)words, mask));
+    *s = (void *)h;
+    return rc;
+}
+
 int xmg_event_elapsed(float *ms, void *e0, void *e1)
 {
     int rc = map(hipEventSynchronize((hipEvent_t)e1));
@@ -374,6 +397,7 @@ const XmhBackend xmh_gpu = {
     xmg_pointer_is_device, xmg_memcpy_peer, xmg_comm_init_all, xmg_comm_destroy, xmg_group_start, xmg_group_end,
     xmg_reduce_scatter_i32, xmg_comm_check, xmg_arch_name, xmg_launch_mix, xmg_launch_mix_window, xmg_launch_fx,
     xmg_launch_mix_placed, xmg_launch_finish_s16, xmg_fast_table_check, xmg_synth, xmg_stream_wait,
+    xmg_stream_create_cus,
 };
 #endif
 

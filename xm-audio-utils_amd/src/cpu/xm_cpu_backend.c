@@ -213,6 +213,15 @@ static int c_stream_wait(void *s, void *e)
     return 0;
 }
 
+/* no CU partitions on the host: a plain stream, and a count of 0 */
+static int c_stream_create_cus(void **s, int lo, int hi, int *n_cus)
+{
+    (void)lo;
+    (void)hi;
+    *n_cus = 0;
+    return s ? c_stream_create(s) : 0;
+}
+
 const XmhBackend xmh_cpu = {
     "cpu",
     c_device_count, c_set_device, c_malloc, c_free, c_malloc, c_free,
@@ -221,4 +230,5 @@ const XmhBackend xmh_cpu = {
     c_pointer_is_device, c_memcpy_peer, c_comm_init_all, c_comm_destroy, c_group, c_group,
     c_reduce_scatter_i32, c_comm_check, c_arch_name, xmc_launch_mix, c_launch_mix_window, xmc_launch_fx,
     xmc_launch_mix_placed, xmc_launch_finish_s16, c_fast_table_check, xmc_synth, c_stream_wait,
+    c_stream_create_cus,
 };

@@ -55,9 +55,11 @@ struct XmAudioMixer {
     XmhGain *unity_dev;            /* one unity-gain descriptor */
     XmMulti *multi;                /* multi-device handle: every call dispatches here */
     /* the time-block pipeline of resample -> biquad cascades -> mix (config 4,
-     * run_fx_pipelined): two internal streams, events per block, the biquad
-     * states and the per-block pointer tables */
-    void *fx_s[2];
+     * run_fx_pipelined): the CU-masked biquad, resample and mix streams (split
+     * fx_k of every 32 CUs), events per block, the biquad states and the
+     * per-block pointer tables */
+    void *fx_s[3];
+    int fx_k;
     void *fx_ev[3][XM_FX_BLOCKS];
     float *fx_state;
     size_t fx_state_cap;
@@ -233,7 +235,7 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
     xmh_free(m->unity_dev);
     xmh_free(m->d_ptrs);
     xmh_host_free(m->h_ptrs);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
         if (m->fx_s[i]) {
             xmh_stream_sync(m->fx_s[i]);
             xmh_stream_destroy(m->fx_s[i]);
@@ -433,15 +435,25 @@ static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *
  * run the chain on each track in place, then the no-resample mix with the
  * track gains.  Order per track: resample -> effects -> gain -> ordered sum. */
 /* Config 4 as a time-block pipeline.  The biquad stage is
- * serial in time and its chain waves hold only a few SIMDs, so the output is
- * cut into XM_FX_BLOCKS blocks of whole 147-output super-periods: block k is
- * resampled on the caller's stream, filtered on fx_s[0] (section states carry
- * from block to block, as in xm_effects_process_stream) once its resample has
- * landed, and mixed on fx_s[1] once filtered.  The resample of block k + 1 and
- * the mix of block k - 1 run beside the biquad of block k.  Every output is
- * the same kernel arithmetic as the three whole-clip passes (window jobs of
- * the same kernels, absolute gain indices), so the result is bit-identical.
- * XM_ENOSYS: not this path's shape (the caller runs the three passes). */
+ * serial in time (sosfilt's order, bit for bit) and its workgroups hold one CU
+ * each (158 KB of LDS) with one latency-bound chain wave, so the output is cut
+ * into XM_FX_BLOCKS blocks of whole 147-output super-periods and the cheap
+ * stages run beside the chain on the CUs it does not use:
+ *   the biquad stream (fx_s[0]) is masked to the CUs i % 32 < k, enough for
+ *   the whole biquad grid at once (k a multiple of 8: the same share of
+ *   every XCD, whose workgroups are dealt round-robin);
+ *   block 0's resample and the last block's mix run on the caller's stream
+ *   over the whole GPU; the other blocks' resamples (fx_s[1]) and mixes
+ *   (fx_s[2]) on the remaining CUs, i % 32 >= k.
+ * Without the masks the resample grids, queued ahead, held every CU's LDS and
+ * the biquad workgroups waited for whole CUs to drain: 10.86 ms against 9.84
+ * for the three passes (profiles/r4_k_configs.jsonl).  Block k is filtered
+ * once its resample has landed (section states carry from block to block, as
+ * in xm_effects_process_stream) and mixed once filtered.  Every output is the
+ * same kernel arithmetic as the three whole-clip passes (window jobs of the
+ * same kernels, absolute gain indices), so the result is bit-identical.
+ * XM_ENOSYS: not this path's shape, or no CU partition fits (the caller runs
+ * the three passes). */
 static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStage *st, int ns, float *scratch,
                             int *launches)
 {
@@ -454,18 +466,46 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
         return XM_ENOSYS;
     if (j0->n_mix > 1 && j0->in_mix_stride != (int64_t)ntr * j0->in_track_stride) return XM_ENOSYS;
     int max_sos = 0;
+    int64_t nwg = 0;   /* biquad workgroups of the largest stage (k_biquad_pc: 16 / n groups of 4 / C clips) */
     for (int s = 0; s < ns; ++s) {
-        if (st[s].kind != 1) return XM_ENOSYS;   /* FIR stages: history handling, the three passes */
+        if (st[s].kind != 1 || st[s].n > 16) return XM_ENOSYS;   /* FIR stages: history handling, the three passes */
         max_sos = st[s].n > max_sos ? st[s].n : max_sos;
+        int kpw = 16 / st[s].n * (4 / C);
+        kpw = kpw < 12 ? kpw : 12;
+        const int64_t w = ((int64_t)ntot + kpw - 1) / kpw;
+        nwg = w > nwg ? w : nwg;
     }
+    /* the CU split: the biquad grid resident at once (two k_biquad_pc
+     * workgroups per CU: 59 KB of LDS each, csrc/xm_fx.hip PC_LDS), the other
+     * CUs for the resample and the mix */
+    int ksplit = 0;
+    for (int k = 8; k < 32 && !ksplit; k += 8) {
+        int nb = 0, nr = 0;
+        xmh_stream_create_cus(NULL, 0, k, &nb);
+        xmh_stream_create_cus(NULL, k, 32, &nr);
+        if (2 * (int64_t)nb >= nwg && nr > 0) ksplit = k;
+    }
+    if (!ksplit) return XM_ENOSYS;
     const int64_t L = m->table.d.L, M = m->table.d.M;
     const int fused = L == 147 && M == 160 && m->table.fast;   /* window jobs of the fused kernel */
     int64_t Fb = (F + XM_FX_BLOCKS - 1) / XM_FX_BLOCKS;
     Fb = (Fb + 146) / 147 * 147;                               /* whole super-periods */
     const int K = (int)((F + Fb - 1) / Fb);
     int rc = XM_OK;
-    for (int i = 0; !rc && i < 2; ++i)
-        if (!m->fx_s[i]) rc = xmh_stream_create(&m->fx_s[i]);
+    if (m->fx_k != ksplit)
+        for (int i = 0; i < 3; ++i)
+            if (m->fx_s[i]) {
+                xmh_stream_sync(m->fx_s[i]);
+                xmh_stream_destroy(m->fx_s[i]);
+                m->fx_s[i] = NULL;
+            }
+    for (int i = 0; !rc && i < 3; ++i)
+        if (!m->fx_s[i]) {
+            int n = 0;
+            rc = xmh_stream_create_cus(&m->fx_s[i], i ? ksplit : 0, i ? 32 : ksplit, &n);
+        }
+    if (rc) return rc;
+    m->fx_k = ksplit;
     for (int a = 0; !rc && a < 3; ++a)
         for (int k = 0; !rc && k < XM_FX_BLOCKS; ++k)
             if (!m->fx_ev[a][k]) rc = xmh_event_create(&m->fx_ev[a][k]);
@@ -497,17 +537,17 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     if (rc) return rc;
     for (int k = 0; k < K; ++k)
         for (size_t i = 0; i < ntot; ++i) m->fx_htab[(size_t)k * ntot + i] = scratch + i * per_track + (size_t)k * Fb * C;
-    void *sb = m->fx_s[0], *sm = m->fx_s[1];
-    /* the biquad stream starts after everything earlier on the caller's stream */
-    rc = xmh_event_record(m->fx_ev[2][0], m->stream);
-    if (!rc) rc = xmh_stream_wait(sb, m->fx_ev[2][0]);
-    if (!rc) rc = xmh_stream_wait(sm, m->fx_ev[2][0]);
+    void *sc = m->stream, *sb = m->fx_s[0], *sr = m->fx_s[1], *sm = m->fx_s[2];
+    /* the internal streams start after everything earlier on the caller's stream */
+    rc = xmh_event_record(m->fx_ev[2][0], sc);
+    for (int i = 0; !rc && i < 3; ++i) rc = xmh_stream_wait(m->fx_s[i], m->fx_ev[2][0]);
     if (!rc) rc = xmh_memcpy_h2d(m->fx_dtab, m->fx_htab, ntab * sizeof(void *), sb);
     if (!rc) rc = xmh_memset(m->fx_state, 0, st_floats * sizeof(float), sb);
     static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
     const int64_t elem = (int64_t)in_bytes(m);
     for (int k = 0; !rc && k < K; ++k) {
         const int64_t o0 = (int64_t)k * Fb, bl = (F - o0) < Fb ? (F - o0) : Fb;
+        void *rs = k == 0 ? sc : sr, *ms = k == K - 1 ? sc : sm;
         /* 1) resample block k of every track (1-track unity mixes) */
         XmhMixJob r = *j0;
         r.n_tracks = 1;
@@ -528,13 +568,13 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
             w.in = (const char *)j0->in + a0 * C * elem;
             w.frames_in = N - a0;
             w.window = a0 > 0;
-            rc = xmh_launch_mix_window(&w, m->stream, launches, &m->timing.fast_launches);
+            rc = xmh_launch_mix_window(&w, rs, launches, &m->timing.fast_launches);
         }
         if (rc == XM_ENOSYS) {   /* any kernel: absolute output window */
             r.out_base = o0;
-            rc = xmh_launch_mix(&r, m->stream, launches, &m->timing.fast_launches);
+            rc = xmh_launch_mix(&r, rs, launches, &m->timing.fast_launches);
         }
-        if (!rc) rc = xmh_event_record(m->fx_ev[0][k], m->stream);
+        if (!rc) rc = xmh_event_record(m->fx_ev[0][k], rs);
         /* 2) the biquad cascades on block k, states carried */
         if (!rc) rc = xmh_stream_wait(sb, m->fx_ev[0][k]);
         for (int s = 0; !rc && s < ns; ++s) {
@@ -552,7 +592,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
         }
         if (!rc) rc = xmh_event_record(m->fx_ev[1][k], sb);
         /* 3) the gained, ordered mix of block k */
-        if (!rc) rc = xmh_stream_wait(sm, m->fx_ev[1][k]);
+        if (!rc) rc = xmh_stream_wait(ms, m->fx_ev[1][k]);
         if (!rc) {
             XmhMixJob x = *j0;
             x.in = scratch + (size_t)o0 * C;
@@ -569,15 +609,15 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
             x.rs.rm = 0;
             x.unity = 0;
             x.rs.fast = 0;
-            rc = xmh_launch_mix(&x, sm, launches, &m->timing.fast_launches);
+            rc = xmh_launch_mix(&x, ms, launches, &m->timing.fast_launches);
         }
     }
-    /* the caller's stream continues after the last mix */
+    /* the caller's stream continues after the other blocks' mixes (the last
+     * block's biquad, which it waited for, follows every resample) */
     if (!rc) rc = xmh_event_record(m->fx_ev[2][1], sm);
-    if (!rc) rc = xmh_stream_wait(m->stream, m->fx_ev[2][1]);
+    if (!rc) rc = xmh_stream_wait(sc, m->fx_ev[2][1]);
     if (rc) {   /* leave nothing in flight on the internal streams */
-        xmh_stream_sync(sb);
-        xmh_stream_sync(sm);
+        for (int i = 0; i < 3; ++i) xmh_stream_sync(m->fx_s[i]);
     }
     return rc;
 }

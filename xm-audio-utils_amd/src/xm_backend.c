@@ -45,6 +45,7 @@ int xmh_event_create(void **e) { return be()->event_create(e); }
 void xmh_event_destroy(void *e) { be()->event_destroy(e); }
 int xmh_event_record(void *e, void *s) { return be()->event_record(e, s); }
 int xmh_stream_wait(void *s, void *e) { return be()->stream_wait(s, e); }
+int xmh_stream_create_cus(void **s, int lo, int hi, int *n_cus) { return be()->stream_create_cus(s, lo, hi, n_cus); }
 int xmh_event_elapsed(float *ms, void *e0, void *e1) { return be()->event_elapsed(ms, e0, e1); }
 int xmh_pointer_is_device(const void *p) { return be()->pointer_is_device(p); }
 
