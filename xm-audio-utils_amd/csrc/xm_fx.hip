@@ -5,11 +5,12 @@
 // sections in order, state zero at clip start.  The recurrence is serial in
 // time, so exactness (SURVEY.md §7 hard part 3) limits the parallelism to
 // clips x sections x channels: k_biquad_pc (cascades of up to 16 sections)
-// gives each (clip, section, channel) its own lane on a chain wave fed by a
-// producer wave, k_biquad_pipe (longer cascades) each (clip, section) with
-// stereo packed; both chain the sections through LDS (see the comments at the
-// kernels).  Earlier designs (k_biquad_lane, the LDS-tap FIR k_fir) and their
-// dev switches left the product in round 4; git history keeps them.
+// gives each (clip, section, channel) its own lane on a chain wave that forms
+// its feed-forward products itself, k_biquad_pipe (longer cascades) each
+// (clip, section) with stereo packed; both chain the sections through LDS (see
+// the comments at the kernels).  Earlier designs (k_biquad_lane, the LDS-tap
+// FIR k_fir, round 3's producer wave) and their dev switches left the product
+// in round 4; git history keeps them.
 // FIR: upfirdn order (_upfirdn.py:107), register-blocked over an LDS tile.
 #include <stdlib.h>
 #include <algorithm>
@@ -925,7 +926,7 @@ extern "C" int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream)
     if (j->n_sos < 1 || j->n_sos > BQ_MAXSEC || (j->channels != 1 && j->channels != 2)) return -1003;
     if (j->n_clips == 0 || j->frames == 0) return 0;
 
-    // cascades of up to 16 sections: producer / chain / load / store waves
+    // cascades of up to 16 sections: chain / load / store waves
     // (k_biquad_pc); longer ones: the section-pipelined k_biquad_pipe
     if (j->n_sos <= 16) {
         auto pk = j->channels == 2 ? (j->state ? k_biquad_pc<2, true> : k_biquad_pc<2, false>)
