@@ -15,7 +15,7 @@
 
 #include "xm_internal.h"
 
-#define XM_FX_BLOCKS 8   /* time blocks of the config-4 pipeline */
+#define XM_FX_BLOCKS 10  /* time blocks of the config-4 pipeline */
 
 struct XmAudioMixer {
     XmMixerConfig cfg;
@@ -462,7 +462,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     const size_t ntot = (size_t)j0->n_mix * (size_t)ntr;
     const size_t per_track = (size_t)F * (size_t)C;
     if (m->cfg.device == XMH_DEV_CPU || ns < 1 || j0->in_ptrs || j0->out_ptrs || j0->io_flags || j0->in_base ||
-        j0->out_base || j0->window || F < 64 * 147 * XM_FX_BLOCKS)
+        j0->out_base || j0->window || F < 32 * 16 * 147)   /* >= 16 super-periods in the smallest block */
         return XM_ENOSYS;
     if (j0->n_mix > 1 && j0->in_mix_stride != (int64_t)ntr * j0->in_track_stride) return XM_ENOSYS;
     int max_sos = 0;
@@ -488,9 +488,19 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     if (!ksplit) return XM_ENOSYS;
     const int64_t L = m->table.d.L, M = m->table.d.M;
     const int fused = L == 147 && M == 160 && m->table.fast;   /* window jobs of the fused kernel */
-    int64_t Fb = (F + XM_FX_BLOCKS - 1) / XM_FX_BLOCKS;
-    Fb = (Fb + 146) / 147 * 147;                               /* whole super-periods */
-    const int K = (int)((F + Fb - 1) / Fb);
+    /* block starts in 32nds of the clip: 1, 2 and 4 at the head (block 0's
+     * resample, on the whole GPU, is all the biquad waits for; each next
+     * resample, on the other CUs, fits inside the block being filtered), 4 in
+     * the body, 3 and 2 at the tail (the last mix runs after the last filter) */
+    static const int cut32[XM_FX_BLOCKS + 1] = {0, 1, 3, 7, 11, 15, 19, 23, 27, 30, 32};
+    int64_t bs[XM_FX_BLOCKS + 1];
+    int K = 0;
+    bs[0] = 0;
+    for (int k = 1; k <= XM_FX_BLOCKS; ++k) {
+        int64_t b = k == XM_FX_BLOCKS ? F : (F * cut32[k] / 32 + 146) / 147 * 147;   /* whole super-periods */
+        b = b > F ? F : b;
+        if (b > bs[K]) bs[++K] = b;
+    }
     int rc = XM_OK;
     if (m->fx_k != ksplit)
         for (int i = 0; i < 3; ++i)
@@ -536,7 +546,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     }
     if (rc) return rc;
     for (int k = 0; k < K; ++k)
-        for (size_t i = 0; i < ntot; ++i) m->fx_htab[(size_t)k * ntot + i] = scratch + i * per_track + (size_t)k * Fb * C;
+        for (size_t i = 0; i < ntot; ++i) m->fx_htab[(size_t)k * ntot + i] = scratch + i * per_track + (size_t)bs[k] * C;
     void *sc = m->stream, *sb = m->fx_s[0], *sr = m->fx_s[1], *sm = m->fx_s[2];
     /* the internal streams start after everything earlier on the caller's stream */
     rc = xmh_event_record(m->fx_ev[2][0], sc);
@@ -546,7 +556,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
     const int64_t elem = (int64_t)in_bytes(m);
     for (int k = 0; !rc && k < K; ++k) {
-        const int64_t o0 = (int64_t)k * Fb, bl = (F - o0) < Fb ? (F - o0) : Fb;
+        const int64_t o0 = bs[k], bl = bs[k + 1] - bs[k];
         void *rs = k == 0 ? sc : sr, *ms = k == K - 1 ? sc : sm;
         /* 1) resample block k of every track (1-track unity mixes) */
         XmhMixJob r = *j0;
