@@ -15,6 +15,14 @@ namespace {
 constexpr int GEN_THREADS = 256;
 constexpr int GEN_OPT = 4;                          // outputs per thread per block
 constexpr int GEN_CHUNK = GEN_THREADS * GEN_OPT;    // output frames per block
+// LDS stride of a phase row of H.  The lanes of a wave read different
+// phases: an even stride put them on a fraction of the banks (T = 44 at
+// 147/320 with 8-B reads: SQ_LDS_BANK_CONFLICT 58 % of the LDS cycles,
+// profiles/r4_v_generic_pmc.json).  T = 4 x odd keeps T and reads 16 B (4
+// taps) at a time, conflict-free bank quads; other even T pad to T + 1 (odd);
+// odd T stays (padding odd T to 4 x odd cost more in table staging and
+// occupancy than it saved: 22.05k -> 48k stereo 9.65 -> 11.2 ms)
+__host__ __device__ inline int gen_row_stride(int T) { return T % 8 == 4 ? T : (T | 1); }
 
 // Input / output layouts and formats (XmhMixJob.io_flags, whole clips only).
 // Input sample (frame f, channel c) of a track of N frames: interleaved at
@@ -59,9 +67,24 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
     const int64_t m1 = min(m0 + GEN_CHUNK, ob + (int64_t)j.frames_out);
     const int64_t N = j.frames_in;
 
-    float *H = lds;                                  // L*T
-    float *tile = lds + ((L * T + 3) & ~3);          // span*C
-    for (int i = threadIdx.x; i < L * T; i += GEN_THREADS) H[i] = j.rs.H[i];
+    const int TH = gen_row_stride(T);
+    float *H = lds;                                  // L*TH
+    float *tile = lds + ((L * TH + 3) & ~3);         // span*C
+    if (TH == T) {
+        for (int i = threadIdx.x; i < L * T; i += GEN_THREADS) H[i] = j.rs.H[i];
+    } else {   // (row, column) of element i carried from one step to the next: two divisions per thread
+        const int dr = GEN_THREADS / T, dc = GEN_THREADS % T;
+        int row = threadIdx.x / T, col = threadIdx.x % T;
+        for (int i = threadIdx.x; i < L * T; i += GEN_THREADS) {
+            H[row * TH + col] = j.rs.H[i];
+            row += dr;
+            col += dc;
+            if (col >= T) {
+                col -= T;
+                ++row;
+            }
+        }
+    }
 
     const int64_t jlo = ((m0 + rm) * M) / L - T + 1;
     const int64_t jhi = ((m1 - 1 + rm) * M) / L;     // inclusive
@@ -87,7 +110,7 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
         for (int o = 0; o < GEN_OPT; ++o) {
             const int u = r0 + (int)(threadIdx.x + o * GEN_THREADS) * M;
             const int qu = u / L;
-            hoff[o] = (u - qu * L) * T;          // phase row of H
+            hoff[o] = (u - qu * L) * TH;         // phase row of H
             xoff[o] = (qb + qu) * C;             // window start in the tile
         }
     }
@@ -129,7 +152,42 @@ __global__ __launch_bounds__(GEN_THREADS) void k_resample_mix_generic(XmhMixJob 
             float r[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) r[c] = 0.0f;
-            for (int t = 0; t < T; ++t) {
+            // stereo taps in blocks of 8: every LDS read of the block issued
+            // before the first product, so one wait covers 8 taps (the
+            // compiler's own unrolling waited for each pair of taps: lgkmcnt(0)
+            // every 4 VALU); same order of ops
+            int t = 0;
+            if constexpr (C == 2) {   // (L, R) as one packed pair: v_pk_mul_f32 + v_pk_add_f32 per tap
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                f2 r2 = f2{0.0f, 0.0f};
+                if (TH % 4 == 0) {   // 16-B rows: the block's coefficients as two ds_read_b128
+                    for (; t + 8 <= T; t += 8) {
+                        typedef float f4 __attribute__((ext_vector_type(4)));
+                        const f4 ha = *(const f4 *)(h + t), hb = *(const f4 *)(h + t + 4);
+                        const float hv[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+                        f2 xv[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) xv[u] = *(const f2 *)(xt + (t + u) * 2);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) r2 = r2 + xv[u] * f2{hv[u], hv[u]};
+                    }
+                } else {
+                    for (; t + 8 <= T; t += 8) {
+                        float hv[8];
+                        f2 xv[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            hv[u] = h[t + u];
+                            xv[u] = *(const f2 *)(xt + (t + u) * 2);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) r2 = r2 + xv[u] * f2{hv[u], hv[u]};
+                    }
+                }
+                r[0] = r2.x;
+                r[1] = r2.y;
+            }
+            for (; t < T; ++t) {
                 const float hv = h[t];
 #pragma unroll
                 for (int c = 0; c < C; ++c) r[c] = r[c] + xt[t * C + c] * hv;
@@ -504,7 +562,7 @@ extern "C" int xmg_launch_mix_generic(const XmhMixJob *j, void *stream, int *n_l
     // this LDS-tile kernel on every ratio measured, 1.4-1.8x; removed.)
     const int64_t L = j->rs.L, M = j->rs.M, T = j->rs.T;
     const int64_t span = (GEN_CHUNK * M) / L + 2 + T;
-    const size_t lds = (size_t)(((L * T + 3) & ~3) + span * C) * sizeof(float);
+    const size_t lds = (size_t)(((L * gen_row_stride((int)T) + 3) & ~3) + span * C) * sizeof(float);
     if (lds > 160 * 1024) return -1003;  // XM_ENOSYS: ratio too extreme for the LDS-staged path
     dim3 grid((unsigned)((j->frames_out + GEN_CHUNK - 1) / GEN_CHUNK), (unsigned)j->n_mix);
     int rc;
