@@ -89,6 +89,49 @@ def test_config4_shard_through_multi_device_handle(xm, gpu):
     _free()
 
 
+def test_config4_time_block_pipeline(xm, gpu):
+    """One device at config 4's clip length: the time-block pipeline (10 blocks
+    of whole super-periods: block resample, biquad with carried states and the
+    gained mix per block, on CU-masked streams; src/xm_audio_mixer.c
+    run_fx_pipelined) is the path taken (30 launches) and every output equals
+    the oracle bit for bit, with ramps and steps that start and end inside
+    blocks and across their edges."""
+    import torch
+    from bench import SEED
+    sos = golden("effects.npz")["sos"]
+    B, ntr, N = 2, 8, 480000
+    F = 441000
+    edge = (F // 32 + 146) // 147 * 147          # the first block edge
+    ramps = [dict(gain0=0.9),
+             dict(gain0=0.0, gain1=0.8, ramp_start=edge - 700, ramp_len=1400),
+             dict(mode=1, ramp_start=3 * edge - 5, ramp_len=9 * edge),
+             dict(gain0=0.3, gain1=0.6, ramp_start=7 * edge),
+             dict(gain0=1.25, gain1=0.5, ramp_start=0, ramp_len=F),
+             dict(gain0=0.5, gain1=0.0, ramp_start=F - 2 * edge - 3, ramp_len=2 * edge),
+             dict(gain0=0.7),
+             dict(gain0=0.2, gain1=0.9, ramp_start=edge, ramp_len=1)]
+    m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
+    m.set_tracks(ramps)
+    e = xm.Effects(44100, 2)
+    for s in sos:
+        e.add_biquad(s)
+    m.set_track_effects(e)
+    assert m.out_frames(N) == F
+    x = torch.empty((B, ntr, N, 2), dtype=torch.float32, device="cuda")
+    xm.synth(x.data_ptr(), "f32", SEED, 77, B * ntr, 2, N)
+    y = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    m.process_strided(x.data_ptr(), N * 2, ntr * N * 2, y.data_ptr(), F * 2, B, N)
+    torch.cuda.synchronize()
+    assert m.timing().n_launches == 30, m.timing().n_launches
+    for b in range(B):
+        xb = x[b].cpu().numpy()
+        r = [CO.biquad_f32(CO.resample_f32(t, 147, 160), sos) for t in xb]
+        assert bits_equal(y[b].cpu().numpy(), CO.mix_f32(r, ramps)), b
+    del x, y
+    _free()
+
+
 def test_config5_production_grid_mix_spanning(xm, gpu):
     import torch
     from bench import RAMPS64, SEED
