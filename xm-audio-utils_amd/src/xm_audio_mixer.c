@@ -15,7 +15,7 @@
 
 #include "xm_internal.h"
 
-#define XM_FX_BLOCKS 10  /* time blocks of the config-4 pipeline */
+#define XM_FX_BLOCKS 8   /* time blocks of the config-4 pipeline */
 
 struct XmAudioMixer {
     XmMixerConfig cfg;
@@ -490,9 +490,10 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     const int fused = L == 147 && M == 160 && m->table.fast;   /* window jobs of the fused kernel */
     /* block starts in 32nds of the clip: 1, 2 and 4 at the head (block 0's
      * resample, on the whole GPU, is all the biquad waits for; each next
-     * resample, on the other CUs, fits inside the block being filtered), 4 in
-     * the body, 3 and 2 at the tail (the last mix runs after the last filter) */
-    static const int cut32[XM_FX_BLOCKS + 1] = {0, 1, 3, 7, 11, 15, 19, 23, 27, 30, 32};
+     * resample, on the other CUs, fits inside the block being filtered), 6 in
+     * the body, 5 and 2 at the tail (the last mix runs after the last filter);
+     * 8 blocks ran 0.7 % faster than 10 with a body of 4 (fewer block starts) */
+    static const int cut32[XM_FX_BLOCKS + 1] = {0, 1, 3, 7, 13, 19, 25, 30, 32};
     int64_t bs[XM_FX_BLOCKS + 1];
     int K = 0;
     bs[0] = 0;
