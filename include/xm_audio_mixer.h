@@ -73,10 +73,16 @@ typedef struct XmMixerConfig {
     int32_t channels;     /* 1 or 2 */
     int32_t sample_fmt;   /* XmSampleFmt, input and output */
     int32_t mem_kind;     /* XmMemKind of the in/out pointers */
-    int32_t device;       /* HIP device ordinal the handle runs on (ignored when n_devices == 0) */
+    int32_t device;       /* HIP device ordinal the handle runs on, or XM_DEVICE_CPU */
     int32_t flags;        /* 0 or XM_MIXER_OUT_CONVERT | XM_MIXER_IN_CONVERT | XM_MIXER_PLANAR */
-    int32_t n_devices;    /* 0: the host CPU backend (XM_DEVICE_CPU);
-                             1: one GPU, `device`; n > 1: GPUs device .. device+n-1 */
+    int32_t n_devices;    /* 0: the host CPU backend (SURVEY.md §8(b) "n_devices (0 = CPU)");
+                             1: one GPU, `device` (XM_DEVICE_CPU: the CPU backend);
+                             n > 1: GPUs device .. device+n-1.
+                             ABI note (round 4 -> 5): before round 4, 0 meant one GPU.  A
+                             CPU handle takes host pointers; with XM_MEM_DEVICE it must be
+                             asked for explicitly (device = XM_DEVICE_CPU): n_devices 0 with
+                             a GPU ordinal and XM_MEM_DEVICE is refused (XM_EINVAL), so a
+                             zero-initialised config can never hand HBM pointers to the host */
 } XmMixerConfig;
 
 typedef struct XmTrackDesc {
@@ -94,12 +100,15 @@ typedef struct XmMixerTiming {
     float kernel_ms;      /* all device compute of the call */
     float d2h_ms;         /* device->host copy-back (XM_MEM_HOST only) */
     int32_t n_launches;   /* kernels launched by the call */
-    int32_t fast_launches; /* of those, launches of the fused 48k->44.1k stereo f32
-                             kernel (k_rs147_mix); the others ran a generic kernel */
+    int32_t fast_launches; /* of those, launches of the fused super-period kernel
+                             (k_rs147_mix: every ratio, layout and format it is
+                             instantiated for); the others ran a
+                             generic kernel */
 } XmMixerTiming;
 
 /* Create a mixer.  Returns NULL on failure; *status (if non-NULL) gets the
- * reason.  n_devices == 0 creates it on the host CPU backend (XM_DEVICE_CPU:
+ * reason.  n_devices == 0 (or device == XM_DEVICE_CPU with n_devices <= 1)
+ * creates it on the host CPU backend (XM_DEVICE_CPU:
  * every call runs on the host cores, in place on host pointers, with the
  * GPU's results bit for bit; no GPU needed).  n_devices >= 1 creates it on
  * GPUs and fails with XM_EDEVICE when they are not usable: a GPU handle never

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 5, box pass c: what the product's other traffic does to its DMA stream
+# (microbenchmark modes), and the store ablations of the fused kernel.
+set -o pipefail
+mkdir -p gpurun_out/r5c
+timeout -k 10 200 python -u -m pytest tests/test_gpu_api_edges.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r5c/pytest_edges.txt 2>&1 || { tail -30 gpurun_out/r5c/pytest_edges.txt; exit 1; }
+tail -2 gpurun_out/r5c/pytest_edges.txt
+timeout -k 10 300 tools/ubench/bin/dma_pattern modes > gpurun_out/r5c/dma_modes.txt 2>&1 || { cat gpurun_out/r5c/dma_modes.txt; exit 1; }
+cat gpurun_out/r5c/dma_modes.txt
+tools/ab_libs.sh 1 lib lib_abnostore lib_abnotaps lib_abnotapsnostore lib_abnodma 2>&1 | tee gpurun_out/r5c/ab.txt || exit 1

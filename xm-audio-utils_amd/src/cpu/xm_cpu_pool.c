@@ -7,6 +7,10 @@
  * handed out one at a time from an atomic counter, so uneven items balance.
  * One parallel region runs at a time; a region started while another runs
  * (another handle on another thread, or a nested call) runs on its caller.
+ * Fork-safe: a child of fork() has none of the parent's workers, so a
+ * pthread_atfork handler resets the pool's locks there and the child's first
+ * parallel region starts its own workers (Python multiprocessing's fork
+ * start method after a CPU-backend call in the parent).
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -21,6 +25,8 @@
 static struct {
     pthread_once_t once;
     int n;                        /* threads including the caller */
+    int want;                     /* threads asked for (XM_CPU_THREADS or the affinity mask) */
+    int spawn;                    /* 1: workers still to be started (first use, or a forked child) */
     pthread_mutex_t mu, region;
     pthread_cond_t go, done;
     unsigned long gen;
@@ -29,7 +35,7 @@ static struct {
     void *ctx;
     int64_t n_items;
     _Atomic int64_t next;
-} P = {PTHREAD_ONCE_INIT, 0, PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER,
+} P = {PTHREAD_ONCE_INIT, 0, 0, 0, PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER,
        PTHREAD_COND_INITIALIZER, 0, 0, NULL, NULL, 0, 0};
 
 static void drain(XmcItemFn fn, void *ctx, int64_t n)
@@ -60,6 +66,37 @@ static void *worker(void *arg)
     return NULL;
 }
 
+/* start the workers (P.mu held or no worker running yet) */
+static void spawn_workers(void)
+{
+    P.n = 1;
+    for (int i = 1; i < P.want; ++i) {
+        pthread_t t;
+        pthread_attr_t at;
+        pthread_attr_init(&at);
+        pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+        const int rc = pthread_create(&t, &at, worker, NULL);
+        pthread_attr_destroy(&at);
+        if (rc) break;   /* fewer threads than asked: still correct */
+        P.n++;
+    }
+    P.spawn = 0;
+}
+
+/* fork() child: only the forking thread exists; the parent's workers, and any
+ * lock one of them held, are gone */
+static void atfork_child(void)
+{
+    pthread_mutex_init(&P.mu, NULL);
+    pthread_mutex_init(&P.region, NULL);
+    pthread_cond_init(&P.go, NULL);
+    pthread_cond_init(&P.done, NULL);
+    P.gen = 0;
+    P.busy = 0;
+    P.n = 1;
+    P.spawn = 1;
+}
+
 static void init_pool(void)
 {
     int n = 0;
@@ -72,22 +109,24 @@ static void init_pool(void)
     }
     if (n < 1) n = 1;
     if (n > XMC_MAX_THREADS) n = XMC_MAX_THREADS;
-    P.n = 1;
-    for (int i = 1; i < n; ++i) {
-        pthread_t t;
-        pthread_attr_t at;
-        pthread_attr_init(&at);
-        pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
-        const int rc = pthread_create(&t, &at, worker, NULL);
-        pthread_attr_destroy(&at);
-        if (rc) break;   /* fewer threads than asked: still correct */
-        P.n++;
-    }
+    P.want = n;
+    spawn_workers();
+    pthread_atfork(NULL, NULL, atfork_child);
+}
+
+/* a forked child's first use starts its own workers (under the region lock) */
+static void respawn_if_forked(void)
+{
+    if (!P.spawn) return;
+    pthread_mutex_lock(&P.region);
+    if (P.spawn) spawn_workers();
+    pthread_mutex_unlock(&P.region);
 }
 
 int xmc_threads(void)
 {
     pthread_once(&P.once, init_pool);
+    respawn_if_forked();
     return P.n;
 }
 
@@ -95,6 +134,7 @@ int xmc_parallel(int64_t n, XmcItemFn fn, void *ctx)
 {
     if (n <= 0) return 0;
     pthread_once(&P.once, init_pool);
+    respawn_if_forked();
     if (P.n == 1 || n == 1 || pthread_mutex_trylock(&P.region) != 0) {
         for (int64_t i = 0; i < n; ++i) fn(ctx, i);   /* serial: one item, one thread, or the pool is busy */
         return 0;

@@ -114,12 +114,21 @@ static int grow(void **p, size_t *cap, size_t need)
     return XM_OK;
 }
 
+/* The host CPU backend (SURVEY.md §8(b) "n_devices (0 = CPU)"): n_devices ==
+ * 0, or device == XM_DEVICE_CPU with n_devices <= 1. */
+static int cfg_cpu(const XmMixerConfig *cfg) { return cfg->n_devices == 0 || (cfg->device == XM_DEVICE_CPU && cfg->n_devices <= 1); }
+
 static int cfg_valid(const XmMixerConfig *cfg)
 {
     return cfg && cfg->in_rate > 0 && cfg->out_rate > 0 && (cfg->channels == 1 || cfg->channels == 2) &&
            (cfg->sample_fmt == XM_FMT_S16 || cfg->sample_fmt == XM_FMT_F32) &&
            (cfg->mem_kind == XM_MEM_HOST || cfg->mem_kind == XM_MEM_DEVICE) &&
-           (cfg->device >= 0 || cfg->n_devices == 0) &&
+           (cfg->device >= 0 || (cfg->device == XM_DEVICE_CPU && cfg_cpu(cfg))) &&
+           /* device memory on the CPU backend must be asked for explicitly
+            * (device = XM_DEVICE_CPU: host memory, used in place); a config
+            * with n_devices 0, a GPU ordinal and XM_MEM_DEVICE would hand HBM
+            * pointers to the host, so it is refused */
+           !(cfg_cpu(cfg) && cfg->mem_kind == XM_MEM_DEVICE && cfg->device != XM_DEVICE_CPU) &&
            !(cfg->flags & ~(int32_t)(XM_MIXER_OUT_CONVERT | XM_MIXER_IN_CONVERT | XM_MIXER_PLANAR)) &&
            cfg->n_devices >= 0 &&
            cfg->n_devices <= XM_MAX_DEVICES;
@@ -173,7 +182,7 @@ XmAudioMixer *xm_audio_mixer_create_ex(const XmMixerConfig *cfg, int *status)
         for (int d = 0; d < cfg->n_devices; ++d) devs[d] = cfg->device + d;
         return xm_audio_mixer_create_multi(cfg, devs, cfg->n_devices, status);
     }
-    const int cpu = cfg->n_devices == 0;   /* n_devices 0 = the host CPU backend */
+    const int cpu = cfg_cpu(cfg);   /* n_devices 0 = the host CPU backend */
     if (!cpu && cfg->device >= xmh_device_count()) {
         rc = XM_EDEVICE;
         goto out;
@@ -435,8 +444,9 @@ static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *
  * run the chain on each track in place, then the no-resample mix with the
  * track gains.  Order per track: resample -> effects -> gain -> ordered sum. */
 /* Config 4 as a time-block pipeline.  The biquad stage is
- * serial in time (sosfilt's order, bit for bit) and its workgroups hold one CU
- * each (158 KB of LDS) with one latency-bound chain wave, so the output is cut
+ * serial in time (sosfilt's order, bit for bit) and its chain waves hold only
+ * a fraction of the SIMDs (k_biquad_pc: 59 KB of LDS per workgroup, two per
+ * CU, one latency-bound chain wave each), so the output is cut
  * into XM_FX_BLOCKS blocks of whole 147-output super-periods and the cheap
  * stages run beside the chain on the CUs it does not use:
  *   the biquad stream (fx_s[0]) is masked to the CUs i % 32 < k, enough for
@@ -611,7 +621,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
             x.in_ptrs_host = NULL;
             x.in_track_stride = (int64_t)per_track;
             x.in_mix_stride = (int64_t)(per_track * (size_t)ntr);
-            x.frames_in = bl;
+            x.frames_in = o0 + bl;   /* the absolute end: frames outside [0, frames_in) read as zero (xm_shim.h) */
             x.frames_out = bl;
             x.in_base = x.out_base = o0;   /* row 0 of the block is absolute frame o0 (gains at absolute frames) */
             x.out = (char *)j0->out + (size_t)o0 * C * (size_t)out_bytes(m);
@@ -673,6 +683,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     r.out_ptrs = NULL;
     r.out_mix_stride = (int64_t)per_track;
     const void **tp = NULL;   /* host table of the track pointers (irregular strides) */
+    void **dtp = NULL;        /* its device copy: a buffer of its own (m->d_ptrs may hold j0's output table) */
     if (j0->in_ptrs) {
         r.in_ptrs = j0->in_ptrs;   /* same mix-major order */
     } else if (j0->n_mix == 1 || j0->in_mix_stride == (int64_t)ntr * j0->in_track_stride) {
@@ -681,16 +692,15 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     } else {
         /* mixes not ntr tracks apart: every track of the batch through a table */
         const int elem = in_bytes(m);
-        const void *const *din = NULL;
-        void *const *dummy = NULL;
         tp = malloc(sizeof(void *) * ntot);
         if (!tp) rc = XM_ENOMEM;
         for (size_t i = 0; !rc && i < ntot; ++i)
             tp[i] = (const char *)j0->in +
                     ((int64_t)(i / (size_t)ntr) * j0->in_mix_stride + (int64_t)(i % (size_t)ntr) * j0->in_track_stride) *
                         elem;
-        if (!rc) rc = ptr_table(m, tp, ntot, NULL, 0, &din, &dummy);
-        r.in_ptrs = din;
+        if (!rc) rc = xmh_malloc((void **)&dtp, sizeof(void *) * ntot);
+        if (!rc) rc = xmh_memcpy_h2d(dtp, tp, sizeof(void *) * ntot, m->stream);
+        r.in_ptrs = (const void *const *)dtp;
         r.in_ptrs_host = tp;
     }
     if (!rc) rc = xmh_launch_mix(&r, m->stream, launches, &m->timing.fast_launches);
@@ -750,6 +760,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
     xmh_stream_sync(m->stream);
     xmh_free(tmp_ptrs);
     xmh_free(ug);
+    xmh_free(dtp);
     free(tp);
     return rc;
 }

@@ -121,9 +121,9 @@ out:
 XmEffects *xm_effects_create(int rate, int channels, int n_devices)
 {
     XmEffectsConfig c = {rate, channels, XM_MEM_HOST, 0};
+    if (n_devices < 0 || n_devices > XM_MAX_DEVICES) return NULL;
     if (n_devices == 0) c.device = XM_DEVICE_CPU;   /* 0 = the host CPU backend */
     if (n_devices <= 1) return xm_effects_create_ex(&c, NULL);
-    if (n_devices < 1 || n_devices > XM_MAX_DEVICES) return NULL;
     int devs[XM_MAX_DEVICES];
     for (int d = 0; d < n_devices; ++d) devs[d] = d;
     return xm_effects_create_multi(&c, devs, n_devices, NULL);

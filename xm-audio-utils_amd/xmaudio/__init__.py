@@ -240,7 +240,7 @@ class Mixer:
         flags = ((XM_MIXER_OUT_CONVERT if convert_out else 0) | (XM_MIXER_IN_CONVERT if convert_in else 0) |
                  (XM_MIXER_PLANAR if planar else 0))
         if device == "cpu":
-            device, n_devices = 0, 0
+            device, n_devices = XM_DEVICE_CPU, 0
         cfg = XmMixerConfig(in_rate, out_rate, channels, FMT[fmt], MEM[mem], device, flags, n_devices)
         st = C.c_int(0)
         if devices is not None:
