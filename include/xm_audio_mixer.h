@@ -265,6 +265,16 @@ XM_API int xm_audio_mixer_get_timing(const XmAudioMixer *m, XmMixerTiming *t);
 /* Destroy and NULL the handle (no-op on NULL). */
 XM_API void xm_audio_mixer_freep(XmAudioMixer **m);
 
+/* Diagnostics (tests): the super-period split of the calling thread's last
+ * launch of the fused kernel k_rs147_mix.  *sp_per_lane = R,
+ * the consecutive super-periods each lane walks (mono kernels: both halves of
+ * the run, 2 x the SPs a lane iterates); *tasks_per_mix = waves per mix (per
+ * group of mixes for the several-mixes-per-wave layouts).  XM_ENOSYS when
+ * this thread has launched no fused kernel (CPU handles never do).  The
+ * environment variable XM_FAST_SPLIT_R=R forces R (rounded up to what the
+ * layout needs) so that small batches exercise the cross-SP paths. */
+XM_API int xm_audio_mixer_last_fast_split(int *sp_per_lane, int *tasks_per_mix);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,7 +3,7 @@
 # (microbenchmark modes), and the store ablations of the fused kernel.
 set -o pipefail
 mkdir -p gpurun_out/r5c
-timeout -k 10 200 python -u -m pytest tests/test_gpu_api_edges.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r5c/pytest_edges.txt 2>&1 || { tail -30 gpurun_out/r5c/pytest_edges.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_api_edges.py tests/test_gpu_fast_multisp.py -x -v -q --timeout 120 --timeout-method thread > gpurun_out/r5c/pytest_edges.txt 2>&1 || { tail -30 gpurun_out/r5c/pytest_edges.txt; exit 1; }
 tail -2 gpurun_out/r5c/pytest_edges.txt
 timeout -k 10 300 tools/ubench/bin/dma_pattern modes > gpurun_out/r5c/dma_modes.txt 2>&1 || { cat gpurun_out/r5c/dma_modes.txt; exit 1; }
 cat gpurun_out/r5c/dma_modes.txt

@@ -66,6 +66,7 @@ EXPORTED = [
     "xm_audio_mixer_process_timeline",
     "xm_audio_mixer_create_multi", "xm_audio_mixer_n_devices", "xm_audio_mixer_process_sharded",
     "xm_audio_mixer_mix_spanning_s16", "xm_effects_create_multi", "xm_effects_n_devices",
+    "xm_audio_mixer_last_fast_split",
 ]
 
 
@@ -148,12 +149,22 @@ _sigs = {
     "xm_effects_create": (_vp, [_i, _i, _i]),
     "xm_effects_create_multi": (_vp, [C.POINTER(XmEffectsConfig), C.POINTER(_i), _i, C.POINTER(_i)]),
     "xm_effects_n_devices": (_i, [_vp]),
+    "xm_audio_mixer_last_fast_split": (_i, [C.POINTER(_i), C.POINTER(_i)]),
 }
 for _n, (_r, _a) in _sigs.items():
     if os.environ.get("XM_AUDIO_LIB") and not hasattr(_lib, _n):
         continue   # dev: an older ablation build lacks newer entry points
     _f = getattr(_lib, _n)
     _f.restype, _f.argtypes = _r, _a
+
+
+def last_fast_split():
+    """(R, tasks_per_mix) of this thread's last fused-kernel launch
+    (xm_audio_mixer_last_fast_split), or None if it made none."""
+    r, t = C.c_int(0), C.c_int(0)
+    if _lib.xm_audio_mixer_last_fast_split(C.byref(r), C.byref(t)) != 0:
+        return None
+    return r.value, t.value
 
 
 class XmError(RuntimeError):
