@@ -440,6 +440,10 @@ static int upload_gains(XmAudioMixer *m)
 static int ptr_table(XmAudioMixer *m, const void *const *in, size_t n_in, void *const *out, size_t n_out,
                      const void *const **din, void *const **dout);
 
+/* floats from one track's row of the effects scratch to the next: whole 64-B
+ * lines, so every row (and every pipeline block, below) starts on a line */
+static size_t fx_track_stride(int64_t frames, int C) { return ((size_t)frames * (size_t)C + 15) & ~(size_t)15; }
+
 /* Effects path (config 4): resample every track into scratch at unity gain,
  * run the chain on each track in place, then the no-resample mix with the
  * track gains.  Order per track: resample -> effects -> gain -> ordered sum. */
@@ -470,7 +474,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     const int C = j0->channels, ntr = j0->n_tracks;
     const int64_t F = j0->frames_out, N = j0->frames_in;
     const size_t ntot = (size_t)j0->n_mix * (size_t)ntr;
-    const size_t per_track = (size_t)F * (size_t)C;
+    const size_t per_track = fx_track_stride(F, C);
     if (m->cfg.device == XMH_DEV_CPU || ns < 1 || j0->in_ptrs || j0->out_ptrs || j0->io_flags || j0->in_base ||
         j0->out_base || j0->window || F < 32 * 16 * 147)   /* >= 16 super-periods in the smallest block */
         return XM_ENOSYS;
@@ -508,7 +512,11 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     int K = 0;
     bs[0] = 0;
     for (int k = 1; k <= XM_FX_BLOCKS; ++k) {
-        int64_t b = k == XM_FX_BLOCKS ? F : (F * cut32[k] / 32 + 146) / 147 * 147;   /* whole super-periods */
+        /* whole groups of 8 super-periods (1176 outputs): every block starts on
+         * a 64-B boundary of the f32 stereo scratch rows (1176 x 8 B = 147 x 64 B),
+         * so the window jobs' whole-segment stores (k_rs147_mix SEG, sc1)
+         * write each 64-B line once, and the biquad and mix read whole lines */
+        int64_t b = k == XM_FX_BLOCKS ? F : (F * cut32[k] / 32 + 1175) / 1176 * 1176;
         b = b > F ? F : b;
         if (b > bs[K]) bs[++K] = b;
     }
@@ -646,7 +654,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
 static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
 {
     const int C = j0->channels, ntr = j0->n_tracks;
-    const size_t per_track = (size_t)j0->frames_out * (size_t)C;
+    const size_t per_track = fx_track_stride(j0->frames_out, C);
     const size_t ntot = (size_t)j0->n_mix * (size_t)ntr;
     /* FIR stages read neighbours of what they write: they ping-pong between
      * two track buffers; biquad cascades run in place */
