@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_api_edges.py tests/test_gpu
 tail -2 gpurun_out/r5c/pytest_edges.txt
 timeout -k 10 300 tools/ubench/bin/dma_pattern modes > gpurun_out/r5c/dma_modes.txt 2>&1 || { cat gpurun_out/r5c/dma_modes.txt; exit 1; }
 cat gpurun_out/r5c/dma_modes.txt
-tools/ab_libs.sh 1 lib lib_abnostore lib_abnotaps lib_abnotapsnostore lib_abnodma 2>&1 | tee gpurun_out/r5c/ab.txt || exit 1
+tools/ab_libs.sh 1 lib lib_abnt lib_abntns lib_abntnw lib_abntnb lib_abntne lib_abntnc lib_abntp8 lib_abntall lib_abp8 lib_abnodma 2>&1 | tee gpurun_out/r5c/ab.txt || exit 1
 timeout -k 10 300 python3 tools/bench_configs.py c4 --steps 10 --warmup 3 > gpurun_out/r5c/c4.txt 2>&1 || { tail -5 gpurun_out/r5c/c4.txt; exit 1; }
 tail -3 gpurun_out/r5c/c4.txt
 tools/dev/pmc_c4.sh r5c/c4 > gpurun_out/r5c/c4_pmc.txt 2>&1 || { tail -5 gpurun_out/r5c/c4_pmc.txt; exit 1; }
