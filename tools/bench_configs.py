@@ -91,6 +91,43 @@ def parity(args, fn):
     return None if args.no_check else bool(fn())
 
 
+_BOX = None
+
+
+def box_info():
+    """Identifiers of the box and its GPU state, attached to every line
+    (config 2 runs 6.5 ms on some boxes, 8.7 on others).
+    rocm-smi's current clocks (sclk, mclk, fclk, socclk), compute and memory
+    partition modes, board serial / unique id and PCI bus; the device's CU
+    count and arch.  Best effort: a missing tool leaves the field out."""
+    global _BOX
+    if _BOX is not None:
+        return _BOX
+    import subprocess
+    box = {}
+    try:
+        p = torch.cuda.get_device_properties(0)
+        box.update(name=p.name, cus=p.multi_processor_count, arch=getattr(p, "gcnArchName", ""),
+                   mem_gb=round(p.total_memory / 2**30, 1))
+    except Exception as e:  # pragma: no cover - box dependent
+        box["props_error"] = str(e)[:80]
+    for flag in ("--showclocks", "--showcomputepartition", "--showmemorypartition", "--showserial", "--showuniqueid",
+                 "--showbus", "--showpower", "--showmaxpower"):
+        try:
+            r = subprocess.run(["rocm-smi", flag, "--json"], capture_output=True, text=True, timeout=20)
+            d = json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip().startswith("{") else {}
+            for card, kv in d.items():
+                if not isinstance(kv, dict):
+                    continue
+                for k, v in kv.items():
+                    box[k] = v
+                break   # the first card: the one this process uses on a 1-GPU box
+        except Exception as e:  # pragma: no cover
+            box[flag.strip("-") + "_error"] = str(e)[:60]
+    _BOX = box
+    return box
+
+
 def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, launches=None, **extra):
     line = {"config": name, "workload": workload, "value": round(samples / (wall_ms * 1e-3) / 1e6, 1),
             "unit": "Msamples/s", "ms_per_step": round(wall_ms, 4), "kernel_ms": round(ker_ms, 4),
@@ -99,6 +136,7 @@ def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, launches=
                          "achieved_GBps": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 1),
                          "frac": round(alg_bytes / (ker_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
     line.update(extra)
+    line["box"] = box_info()
     print(json.dumps(line), flush=True)
 
 
