@@ -105,12 +105,9 @@ def box_info():
         return _BOX
     import subprocess
     box = {}
-    try:
-        p = torch.cuda.get_device_properties(0)
-        box.update(name=p.name, cus=p.multi_processor_count, arch=getattr(p, "gcnArchName", ""),
-                   mem_gb=round(p.total_memory / 2**30, 1))
-    except Exception as e:  # pragma: no cover - box dependent
-        box["props_error"] = str(e)[:80]
+    # rocm-smi first, from a process that has not touched the GPU yet (main()
+    # calls this before any device work): the box refuses an exec from a
+    # GPU-initialised process, and rocm-smi re-execs its interpreter
     for flag in ("--showclocks", "--showcomputepartition", "--showmemorypartition", "--showserial", "--showuniqueid",
                  "--showbus", "--showpower", "--showmaxpower"):
         try:
@@ -128,6 +125,19 @@ def box_info():
     return box
 
 
+def box_props():
+    """The device's CU count, arch and memory (after the GPU is up)."""
+    box = box_info()
+    if "cus" not in box:
+        try:
+            p = torch.cuda.get_device_properties(0)
+            box.update(name=p.name, cus=p.multi_processor_count, arch=getattr(p, "gcnArchName", ""),
+                       mem_gb=round(p.total_memory / 2**30, 1))
+        except Exception as e:  # pragma: no cover - box dependent
+            box["props_error"] = str(e)[:80]
+    return box
+
+
 def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, launches=None, **extra):
     line = {"config": name, "workload": workload, "value": round(samples / (wall_ms * 1e-3) / 1e6, 1),
             "unit": "Msamples/s", "ms_per_step": round(wall_ms, 4), "kernel_ms": round(ker_ms, 4),
@@ -136,7 +146,7 @@ def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, launches=
                          "achieved_GBps": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 1),
                          "frac": round(alg_bytes / (ker_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
     line.update(extra)
-    line["box"] = box_info()
+    line["box"] = box_props()
     print(json.dumps(line), flush=True)
 
 
@@ -478,7 +488,13 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the post-timing oracle checks")
     ap.add_argument("--clips-fx", type=int, default=1024, help="fir / bq: clips")
     ap.add_argument("--fir-k", default="63", help="fir: taps (a comma list: one line each)")
+    ap.add_argument("--no-box", action="store_true",
+                    help="no rocm-smi box identifiers (under rocprofv3, whose preload initialises the GPU first)")
     a = ap.parse_args()
+    global _BOX
+    if a.no_box or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ):   # under rocprofv3: no rocm-smi
+        _BOX = {}
+    box_info()   # before any device work (see box_info)
     for w in a.which:
         globals()[w](a)
         torch.cuda.empty_cache()

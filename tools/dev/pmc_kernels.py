@@ -19,6 +19,7 @@ import os
 
 
 def family(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
     for ch in "<(":
         i = name.find(ch)
         if i > 0:
