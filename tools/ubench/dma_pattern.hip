@@ -39,7 +39,56 @@ __device__ __forceinline__ uint64_t stream_addr(int layout, int w, int q, int j)
     }
 }
 
-template <int PIECE, int POL, int MODE = 0>   // POL 0: nt, 1: default, 2: sc1; MODE bits: 1 the product's output stores, 2 its slot copies, 4 its exchange
+// SM (output store forms, MODE & 1; the product issues 19 rounds per 5 segments,
+// lane (slot lane / 8, output lane % 8) of each round's 8 outputs per slot):
+//   0 b64 per round, default policy (the product)   1 the same, sc1   2 the same, nt
+//   3 b128 per 2 rounds (one whole 128-B piece per slot), default   4 that, sc1   5 that, nt
+//   6 256 B per slot per 4 rounds (two b128 instructions), default
+//   7 b64 per round, slots on interleaved super-periods (a round's 8 pieces within 9.4 KB)
+template <int SM>
+__device__ __forceinline__ void out_stores(int k, int w, int lane, __amdgpu_buffer_rsrc_t ro, float acc)
+{
+    const int mix = w >> 2, task = w & 3;
+    const int r0 = (k * 19) / 5, r1 = ((k + 1) * 19) / 5;
+    const uint32_t ob = 0;   // the resource is based at the wave's mix output
+    const uint32_t run = 94u * 147u;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    for (int r = r0; r < r1; ++r) {
+        if constexpr (SM <= 2 || SM == 7) {
+            const int sl = lane >> 3, kk = lane & 7;
+            uint32_t n = (uint32_t)(task * 8 + sl) * run + (uint32_t)r * 8 + kk;
+            if constexpr (SM == 7) n = (uint32_t)task * 8 * run + (uint32_t)((r / 19) * 8 + sl) * 147 + (uint32_t)(r % 19) * 8 + kk;
+            __builtin_amdgcn_raw_buffer_store_b64(f2v{acc, acc}, ro, ob + n * 8u, 0, SM == 1 ? 16 : SM == 2 ? 2 : 0);
+        } else if constexpr (SM <= 5) {
+            if (r & 1) {
+                const int sl = lane >> 3, e = lane & 7;
+                const uint32_t n = (uint32_t)(task * 8 + sl) * run + (uint32_t)(r - 1) * 8 + 2 * e;
+                __builtin_amdgcn_raw_buffer_store_b128(f4v{acc, acc, acc, acc}, ro, ob + n * 8u, 0, SM == 4 ? 16 : SM == 5 ? 2 : 0);
+            }
+        } else if constexpr (SM == 9 || SM == 10) {   // the product's pieces, every wave inside a 16-KB (9) or 1-KB (10) footprint
+            const int sl = lane >> 3, kk = lane & 7;
+            const uint32_t n = SM == 9 ? (uint32_t)task * 2048u + (uint32_t)sl * 256u + (uint32_t)((r * 8 + kk) & 255)
+                                       : (uint32_t)task * 128u + (uint32_t)sl * 16u + (uint32_t)((r * 8 + kk) & 15);
+            __builtin_amdgcn_raw_buffer_store_b64(f2v{acc, acc}, ro, ob + n * 8u, 0, 0);
+        } else if constexpr (SM == 8) {   // wave-private contiguous output, 1 KiB per instruction, ~1 per 2 rounds
+            if (r & 1) {
+                const uint32_t n = (uint32_t)task * 8 * run + (uint32_t)(r >> 1) * 128 + 2 * lane;
+                __builtin_amdgcn_raw_buffer_store_b128(f4v{acc, acc, acc, acc}, ro, ob + n * 8u, 0, 0);
+            }
+        } else {
+            if ((r & 3) == 3) {
+                for (int i = 0; i < 2; ++i) {
+                    const int sl = 4 * i + (lane >> 4), e = lane & 15;
+                    const uint32_t n = (uint32_t)(task * 8 + sl) * run + (uint32_t)(r - 3) * 8 + 2 * e;
+                    __builtin_amdgcn_raw_buffer_store_b128(f4v{acc, acc, acc, acc}, ro, ob + n * 8u, 0, 0);
+                }
+            }
+        }
+    }
+}
+
+template <int PIECE, int POL, int MODE = 0, int SM = 0>   // POL 0: nt, 1: default, 2: sc1; MODE bits: 1 the product's output stores, 2 its slot copies, 4 its exchange
 __global__ __launch_bounds__(512) void k_dma(const char *buf, int layout, int delay, unsigned *sink, char *obuf)
 {
     extern __shared__ __attribute__((aligned(16))) char lds_all[];
@@ -64,36 +113,35 @@ __global__ __launch_bounds__(512) void k_dma(const char *buf, int layout, int de
     constexpr int SPI = 64 / LPS;            // streams per instruction
     constexpr int SEGP = PIECE / 256;        // segments per piece
     float acc = 0.0f;
+    [[maybe_unused]] float4 regs[16];
     // every step moves 16 KiB (16 instructions): with larger pieces a step
     // covers 64 / SEGP of the streams, in turn
 #pragma unroll 1
     for (int k = 0; k < NSEG; ++k) {
         const int j = k / SEGP * SEGP, gsel = k % SEGP;
 #pragma unroll
-        for (int d = 0; d < 16; ++d) {
+        for (int d = 0; d < ((MODE & 16) ? 0 : 16); ++d) {   // MODE 16: no DMA (the stores alone)
             const int q = gsel * (64 / SEGP) + d * SPI + lane / LPS;
             const int c = lane % LPS;        // 16-B chunk within the piece
             const uint32_t off = (uint32_t)(stream_addr(layout, w, q, j + c / 16) - lo) + (uint32_t)(c % 16) * 16u;
             const uint32_t m0 = ldsb + (uint32_t)d * 1024u;
-            if constexpr (POL == 0)
+            if constexpr (POL == 3) {   // plain loads into registers (no LDS-DMA)
+                float4 v;
+                asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+                regs[d] = v;
+            } else if constexpr (POL == 0)
                 asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds" ::"s"(m0), "v"(off), "s"(rs) : "memory", "m0");
             else if constexpr (POL == 1)
                 asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(rs) : "memory", "m0");
             else
                 asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen sc1 lds" ::"s"(m0), "v"(off), "s"(rs) : "memory", "m0");
         }
-        if constexpr (MODE & 1) {
-            // 19 rounds per 5 segments: ~4 b64 stores per step, lane (slot
-            // lane / 8, output lane % 8) of the round's 8 outputs per slot
-            const int mix = w >> 2, task = w & 3, sl = lane >> 3, kk = lane & 7;
-            const uint64_t ob = (uint64_t)mix * 441000 * 8;
-            for (int i = 0; i < 4; ++i) {
-                const int r = (k * 19) / 5 + i;   // rounds advance 3.8 per segment (overlap at the edges is harmless)
-                const uint64_t o = ob + ((uint64_t)(task * 8 + sl) * 94 * 147 + (uint64_t)r * 8 + kk) * 8;
-                if (o + 8 <= (uint64_t)512 * 441000 * 8) *(float2 *)(obuf + o) = make_float2(acc, acc);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (MODE & 1)
+            out_stores<SM>(k, w, lane, __builtin_amdgcn_make_buffer_rsrc(obuf + (size_t)(w >> 2) * 441000u * 8u, (short)0, (int)(441000u * 8u), 0x00020000), acc);
+        if constexpr (MODE & 8)   // the step's stores younger than its DMA: wait for the DMA only (<= 4 stores after it)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (MODE & 2) {   // the slot -> register copy: 16 ds_read_b128 per segment
             float4 t = float4{0, 0, 0, 0};
 #pragma unroll
@@ -120,6 +168,10 @@ __global__ __launch_bounds__(512) void k_dma(const char *buf, int layout, int de
             acc += t.x;
         }
         acc += *(const float *)(slot + lane * 16);
+        if constexpr (POL == 3) {
+#pragma unroll
+            for (int d = 0; d < 16; ++d) acc += regs[d].x;
+        }
         for (int i = 0; i < delay; ++i) __builtin_amdgcn_s_sleep(8);
     }
     if (acc == 1234.5f) sink[0] = 1;
@@ -158,6 +210,32 @@ int main(int argc, char **argv)
         printf("%-10s layout %d delay %3d: %8.3f ms %8.1f GB/s\n", name, layout, delay, best, moved / (best * 1e-3) / 1e9);
         fflush(stdout);
     };
+    if (argc > 1 && argv[1][0] == 's') {   // output store forms beside the stream
+        run(k_dma<256, 0, 0>, "no stores", 0, 0);
+        run(k_dma<256, 0, 1, 0>, "b64 def", 0, 0);
+        run(k_dma<256, 0, 1, 1>, "b64 sc1", 0, 0);
+        run(k_dma<256, 0, 1, 2>, "b64 nt", 0, 0);
+        run(k_dma<256, 0, 1, 3>, "b128 def", 0, 0);
+        run(k_dma<256, 0, 1, 4>, "b128 sc1", 0, 0);
+        run(k_dma<256, 0, 1, 5>, "b128 nt", 0, 0);
+        run(k_dma<256, 0, 1, 6>, "256B def", 0, 0);
+        run(k_dma<256, 0, 1, 7>, "b64 ilv", 0, 0);
+        run(k_dma<256, 1, 1, 0>, "b64 def, def loads", 0, 0);
+        run(k_dma<256, 0, 9, 0>, "b64 def, acks not waited", 0, 0);
+        run(k_dma<256, 0, 9, 3>, "b128 def, acks not waited", 0, 0);
+        run(k_dma<256, 0, 9, 0>, "b64 def, acks not waited", 0, 8);
+        run(k_dma<256, 0, 1, 8>, "1K contiguous", 0, 0);
+        run(k_dma<256, 0, 1, 9>, "b64 small footprint", 0, 0);
+        run(k_dma<256, 0, 1, 10>, "b64 1K footprint", 0, 0);
+        run(k_dma<256, 3, 0, 0>, "VGPR loads, no stores", 0, 0);
+        run(k_dma<256, 3, 1, 0>, "VGPR loads + b64 stores", 0, 0);
+        run(k_dma<256, 0, 0, 0>, "coalesced, no stores", 2, 0);
+        run(k_dma<256, 0, 1, 0>, "coalesced + b64 stores", 2, 0);
+        run(k_dma<256, 0, 1, 8>, "coalesced + 1K stores", 2, 0);
+        run(k_dma<256, 0, 17, 0>, "b64 stores alone", 0, 0);
+        run(k_dma<256, 0, 17, 8>, "1K contig stores alone", 0, 0);
+        return 0;
+    }
     if (argc > 1) {   // the product's other traffic beside its DMA stream
         run(k_dma<256, 0, 0>, "base", 0, 0);
         run(k_dma<256, 0, 1>, "+stores", 0, 0);
