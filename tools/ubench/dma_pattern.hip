@@ -60,6 +60,11 @@ __device__ __forceinline__ void out_stores(int k, int w, int lane, __amdgpu_buff
             uint32_t n = (uint32_t)(task * 8 + sl) * run + (uint32_t)r * 8 + kk;
             if constexpr (SM == 7) n = (uint32_t)task * 8 * run + (uint32_t)((r / 19) * 8 + sl) * 147 + (uint32_t)(r % 19) * 8 + kk;
             __builtin_amdgcn_raw_buffer_store_b64(f2v{acc, acc}, ro, ob + n * 8u, 0, SM == 1 ? 16 : SM == 2 ? 2 : 0);
+        } else if constexpr (SM >= 11 && SM <= 15) {   // b64 per round, other cache-policy bits: sc0, sc0|sc1, sc0|nt, nt|sc1, all three
+            const int sl = lane >> 3, kk = lane & 7;
+            const uint32_t n = (uint32_t)(task * 8 + sl) * run + (uint32_t)r * 8 + kk;
+            constexpr int AUX = SM == 11 ? 1 : SM == 12 ? 17 : SM == 13 ? 3 : SM == 14 ? 18 : 19;
+            __builtin_amdgcn_raw_buffer_store_b64(f2v{acc, acc}, ro, ob + n * 8u, 0, AUX);
         } else if constexpr (SM <= 5) {
             if (r & 1) {
                 const int sl = lane >> 3, e = lane & 7;
@@ -210,6 +215,17 @@ int main(int argc, char **argv)
         printf("%-10s layout %d delay %3d: %8.3f ms %8.1f GB/s\n", name, layout, delay, best, moved / (best * 1e-3) / 1e9);
         fflush(stdout);
     };
+    if (argc > 1 && argv[1][0] == 'p') {   // store cache-policy bits
+        run(k_dma<256, 0, 0>, "no stores", 0, 0);
+        run(k_dma<256, 0, 1, 0>, "b64 def", 0, 0);
+        run(k_dma<256, 0, 1, 11>, "b64 sc0", 0, 0);
+        run(k_dma<256, 0, 1, 12>, "b64 sc0 sc1", 0, 0);
+        run(k_dma<256, 0, 1, 13>, "b64 sc0 nt", 0, 0);
+        run(k_dma<256, 0, 1, 14>, "b64 sc1 nt", 0, 0);
+        run(k_dma<256, 0, 1, 15>, "b64 sc0 sc1 nt", 0, 0);
+        run(k_dma<256, 2, 1, 0>, "sc1 loads + b64 def", 0, 0);
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 's') {   // output store forms beside the stream
         run(k_dma<256, 0, 0>, "no stores", 0, 0);
         run(k_dma<256, 0, 1, 0>, "b64 def", 0, 0);
