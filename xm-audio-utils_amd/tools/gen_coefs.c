@@ -9,7 +9,8 @@
  * coefficient inline (no scalar loads).  Tap 22 of every phase must be an exact
  * zero (the 160-frame pre-pad); the generator refuses otherwise.
  *
- * and the 44.1k->48k tables (emit_up), and the small-ratio pair tables
+ * and the 44.1k->48k tables (emit_up), the 44.1k->96k / 22.05k->48k ones
+ * (emit_offsets "U2": L/M = 320/147), and the small-ratio pair tables
  * (emit_ratio: 3/2, 2/3, 1/2, 2/1, 3/1).
  *
  * usage: gen_coefs <out.h>
@@ -28,55 +29,69 @@
  * gets +0 coefficients past its end (acc + x*0 == acc up to the sign of zero,
  * which the kernel's final + 0 fixes; finite inputs), and the leading zero
  * taps are dropped like the 147/160 kernel's tap 22. */
-static int emit_up(FILE *f)
+/* The same per-output used-tap runs for any L (even) / M with T = 21 (emit_up
+ * for 160/147; 320/147 = 44.1k -> 96k and 22.05k -> 48k as "U2"): emits
+ * XM_FAST_RM_<sfx>, kOff<sfx>[L], kPt<sfx>[L / 2] and XM_KHP<sfx>_INIT[L / 2 +
+ * 1][42]. */
+static int emit_offsets(FILE *f, const char *sfx, int in_rate, int out_rate, int Lx, int Mx)
 {
     XmResampleDesign d;
-    static float H[160 * 21];
-    if (xm_resample_design(44100, 48000, &d, NULL) || d.L != 160 || d.M != 147 || d.T != 21 ||
-        xm_resample_design(44100, 48000, &d, H)) {
-        fprintf(stderr, "gen_coefs: unexpected 44.1k->48k design\n");
-        return 1;
+    float *H = calloc((size_t)Lx * 21, sizeof(float));
+    int *off = calloc((size_t)Lx, sizeof(int)), *n = calloc((size_t)Lx, sizeof(int)), *pt = calloc((size_t)Lx / 2, sizeof(int));
+    int rc = 1;
+    if (!H || !off || !n || !pt || xm_resample_design(in_rate, out_rate, &d, NULL) || d.L != Lx || d.M != Mx ||
+        d.T != 21 || xm_resample_design(in_rate, out_rate, &d, H)) {
+        fprintf(stderr, "gen_coefs: unexpected %d -> %d design\n", in_rate, out_rate);
+        goto out;
     }
-    int off[160], n[160], pt[80];
-    for (int k = 0; k < 160; ++k) {
-        const int ph = ((k + d.rm) * 147) % 160;
+    for (int k = 0; k < Lx; ++k) {
+        const int ph = (int)(((long)(k + d.rm) * Mx) % Lx);
         int lo = -1, hi = -1;
         for (int t = 0; t < 21; ++t)
             if (H[ph * 21 + t] != 0.0f) {
                 if (lo < 0) lo = t;
                 hi = t;
             }
-        if (lo < 0) return 1;
+        if (lo < 0) goto out;
         off[k] = lo;   /* interior zero taps, if any, stay in the chain */
         n[k] = hi - lo + 1;
     }
-    for (int i = 0; i < 80; ++i) {
+    for (int i = 0; i < Lx / 2; ++i) {
         pt[i] = n[2 * i] > n[2 * i + 1] ? n[2 * i] : n[2 * i + 1];
         if (pt[i] < 17 || pt[i] > 21) {
-            fprintf(stderr, "gen_coefs: pair %d runs %d taps\n", i, pt[i]);
-            return 1;
+            fprintf(stderr, "gen_coefs: %s pair %d runs %d taps\n", sfx, i, pt[i]);
+            goto out;
         }
     }
-    fprintf(f, "// 44.1k -> 48k (xm_resample_design(44100, 48000)): L = 160, M = 147, T = 21\n");
-    fprintf(f, "#define XM_FAST_RM_UP %d\n", d.rm);
-    fprintf(f, "static constexpr int kOffU[160] = {");
-    for (int k = 0; k < 160; ++k) fprintf(f, "%s%d", k ? ", " : "", off[k]);
-    fprintf(f, "};\nstatic constexpr int kPtU[80] = {");
-    for (int i = 0; i < 80; ++i) fprintf(f, "%s%d", i ? ", " : "", pt[i]);
-    fprintf(f, "};\n#define XM_KHPU_INIT { \\\n");
-    for (int i = 0; i < 81; ++i) {   /* + 1 zero row: prefetch past the end stays in bounds */
+    fprintf(f, "// %d -> %d (xm_resample_design(%d, %d)): L = %d, M = %d, T = 21\n", in_rate, out_rate, in_rate,
+            out_rate, Lx, Mx);
+    fprintf(f, "#define XM_FAST_RM_%s %d\n", sfx, d.rm);
+    fprintf(f, "static constexpr int kOff%s[%d] = {", sfx, Lx);
+    for (int k = 0; k < Lx; ++k) fprintf(f, "%s%d", k ? ", " : "", off[k]);
+    fprintf(f, "};\nstatic constexpr int kPt%s[%d] = {", sfx, Lx / 2);
+    for (int i = 0; i < Lx / 2; ++i) fprintf(f, "%s%d", i ? ", " : "", pt[i]);
+    fprintf(f, "};\n#define XM_KHP%s_INIT { \\\n", sfx);
+    for (int i = 0; i <= Lx / 2; ++i) {   /* + 1 zero row: prefetch past the end stays in bounds */
         fprintf(f, "  {");
         for (int e = 0; e < 21; ++e)
             for (int j = 0; j < 2; ++j) {
                 const int k = 2 * i + j;
-                const float v = k < 160 && e < n[k] ? H[(((k + d.rm) * 147) % 160) * 21 + off[k] + e] : 0.0f;
+                const float v = k < Lx && e < n[k] ? H[(int)(((long)(k + d.rm) * Mx) % Lx) * 21 + off[k] + e] : 0.0f;
                 fprintf(f, "%s%af", e || j ? ", " : "", (double)v);
             }
         fprintf(f, "}, \\\n");
     }
     fprintf(f, "}\n");
-    return 0;
+    rc = 0;
+out:
+    free(H);
+    free(off);
+    free(n);
+    free(pt);
+    return rc;
 }
+
+static int emit_up(FILE *f) { return emit_offsets(f, "U", 44100, 48000, 160, 147); }
 
 /* The small-L/M ratios of the fused kernel (RatioBase<RID> in
  * csrc/xm_resample_fast.hip): every output runs all T taps, and the phase of
@@ -163,7 +178,7 @@ int main(int argc, char **argv)
         fprintf(f, "}, \\\n");
     }
     fprintf(f, "}\n");
-    return emit_up(f) || emit_ratio(f, "32", 3, 2) || emit_ratio(f, "23", 2, 3) || emit_ratio(f, "12", 1, 2) ||
+    return emit_up(f) || emit_offsets(f, "U2", 44100, 96000, 320, 147) || emit_ratio(f, "32", 3, 2) || emit_ratio(f, "23", 2, 3) || emit_ratio(f, "12", 1, 2) ||
                    emit_ratio(f, "21", 2, 1) || emit_ratio(f, "31", 3, 1) || fclose(f)
                ? 1
                : 0;
