@@ -84,7 +84,8 @@ LK_SGPR = (96, 98)
 
 
 def lblock(ntaps, first, two):
-    """Packed taps with literal coefficients (TAPS == 3): no scalar memory.
+    """Packed taps with literal coefficients (the LIT kernels, 320/147: the
+    pair table does not fit the scalar cache): no scalar memory.
     Per tap t the coefficient pair (h_k[t], h_k+1[t]) is written into an SGPR
     pair by two s_mov_b32 (SALU, issued between the VALU of the previous tap;
     the two pairs alternate by tap parity) and read by the two v_pk_mul_f32
@@ -141,10 +142,10 @@ for first, n, name in ((True, 8, "G0"), (False, 8, "G1"), (False, 6, "G2")) + tu
         (False, n, f"G2T{n}") for n in (1, 2, 3, 4, 5, 7)):
     for two in (True, False):
         out.append(f'#define XM_PK_{name}_{"TWO" if two else "ONE"} "{block(n, first, two)}"')
-for n in (2, 4):
+for n in (1, 2, 3, 4):
     for first in (True, False):
         for two in (True, False):
-            if first and n == 2:
+            if first and n != 4:
                 continue
             out.append(f'#define XM_LK_{"F" if first else "R"}{n}_{"TWO" if two else "ONE"} "{lblock(n, first, two)}"')
 out.append(f'#define XM_LK_CLOBBER "s{LK_SGPR[0]}", "s{LK_SGPR[0] + 1}", "s{LK_SGPR[1]}", "s{LK_SGPR[1] + 1}"')
