@@ -25,6 +25,9 @@ int xmg_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches);
 int xmg_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
                           int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream);
 int xmg_fast_table_check(const float *H, int L, int M, int T);                   /* xm_resample_fast.hip */
+/* 147/320 (96k -> 44.1k): xm_resample_d2.hip; -1003 when the job is not its shape */
+int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launches, int *R_out, int *tpm_out);
+int xmg_d2_table_check(const float *H, int L, int M, int T);
 int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream);                        /* xm_fx.hip */
 int xmg_launch_fx_fir(const XmhFxJob *j, void *stream);
 int xmg_synth(void *out, int fmt, uint64_t seed, uint64_t clip0, int64_t n_clips, int channels, int64_t frames,

@@ -33,22 +33,30 @@
  * for 160/147; 320/147 = 44.1k -> 96k and 22.05k -> 48k as "U2"): emits
  * XM_FAST_RM_<sfx>, kOff<sfx>[L], kPt<sfx>[L / 2] and XM_KHP<sfx>_INIT[L / 2 +
  * 1][42]. */
+static int emit_offsets_t(FILE *f, const char *sfx, int in_rate, int out_rate, int Lx, int Mx, int Tx, int ptmin, int ptmax);
 static int emit_offsets(FILE *f, const char *sfx, int in_rate, int out_rate, int Lx, int Mx)
 {
+    return emit_offsets_t(f, sfx, in_rate, out_rate, Lx, Mx, 21, 17, 21);
+}
+
+/* any T: also kNum<sfx>[L] (used taps of each output) */
+static int emit_offsets_t(FILE *f, const char *sfx, int in_rate, int out_rate, int Lx, int Mx, int Tx, int ptmin, int ptmax)
+{
     XmResampleDesign d;
-    float *H = calloc((size_t)Lx * 21, sizeof(float));
-    int *off = calloc((size_t)Lx, sizeof(int)), *n = calloc((size_t)Lx, sizeof(int)), *pt = calloc((size_t)Lx / 2, sizeof(int));
+    const int NP = (Lx + 1) / 2;   /* pairs; an odd L leaves the last output unpaired (+0 partner) */
+    float *H = calloc((size_t)Lx * Tx, sizeof(float));
+    int *off = calloc((size_t)Lx, sizeof(int)), *n = calloc((size_t)Lx, sizeof(int)), *pt = calloc((size_t)NP, sizeof(int));
     int rc = 1;
     if (!H || !off || !n || !pt || xm_resample_design(in_rate, out_rate, &d, NULL) || d.L != Lx || d.M != Mx ||
-        d.T != 21 || xm_resample_design(in_rate, out_rate, &d, H)) {
+        d.T != Tx || xm_resample_design(in_rate, out_rate, &d, H)) {
         fprintf(stderr, "gen_coefs: unexpected %d -> %d design\n", in_rate, out_rate);
         goto out;
     }
     for (int k = 0; k < Lx; ++k) {
         const int ph = (int)(((long)(k + d.rm) * Mx) % Lx);
         int lo = -1, hi = -1;
-        for (int t = 0; t < 21; ++t)
-            if (H[ph * 21 + t] != 0.0f) {
+        for (int t = 0; t < Tx; ++t)
+            if (H[ph * Tx + t] != 0.0f) {
                 if (lo < 0) lo = t;
                 hi = t;
             }
@@ -56,27 +64,30 @@ static int emit_offsets(FILE *f, const char *sfx, int in_rate, int out_rate, int
         off[k] = lo;   /* interior zero taps, if any, stay in the chain */
         n[k] = hi - lo + 1;
     }
-    for (int i = 0; i < Lx / 2; ++i) {
-        pt[i] = n[2 * i] > n[2 * i + 1] ? n[2 * i] : n[2 * i + 1];
-        if (pt[i] < 17 || pt[i] > 21) {
+    for (int i = 0; i < NP; ++i) {
+        const int n1 = 2 * i + 1 < Lx ? n[2 * i + 1] : 0;
+        pt[i] = n[2 * i] > n1 ? n[2 * i] : n1;
+        if (pt[i] < ptmin || pt[i] > ptmax) {
             fprintf(stderr, "gen_coefs: %s pair %d runs %d taps\n", sfx, i, pt[i]);
             goto out;
         }
     }
-    fprintf(f, "// %d -> %d (xm_resample_design(%d, %d)): L = %d, M = %d, T = 21\n", in_rate, out_rate, in_rate,
-            out_rate, Lx, Mx);
+    fprintf(f, "// %d -> %d (xm_resample_design(%d, %d)): L = %d, M = %d, T = %d\n", in_rate, out_rate, in_rate,
+            out_rate, Lx, Mx, Tx);
     fprintf(f, "#define XM_FAST_RM_%s %d\n", sfx, d.rm);
     fprintf(f, "static constexpr int kOff%s[%d] = {", sfx, Lx);
     for (int k = 0; k < Lx; ++k) fprintf(f, "%s%d", k ? ", " : "", off[k]);
-    fprintf(f, "};\nstatic constexpr int kPt%s[%d] = {", sfx, Lx / 2);
-    for (int i = 0; i < Lx / 2; ++i) fprintf(f, "%s%d", i ? ", " : "", pt[i]);
+    fprintf(f, "};\nstatic constexpr int kNum%s[%d] = {", sfx, Lx);
+    for (int k = 0; k < Lx; ++k) fprintf(f, "%s%d", k ? ", " : "", n[k]);
+    fprintf(f, "};\nstatic constexpr int kPt%s[%d] = {", sfx, NP);
+    for (int i = 0; i < NP; ++i) fprintf(f, "%s%d", i ? ", " : "", pt[i]);
     fprintf(f, "};\n#define XM_KHP%s_INIT { \\\n", sfx);
-    for (int i = 0; i <= Lx / 2; ++i) {   /* + 1 zero row: prefetch past the end stays in bounds */
+    for (int i = 0; i <= NP; ++i) {   /* + 1 zero row: prefetch past the end stays in bounds */
         fprintf(f, "  {");
-        for (int e = 0; e < 21; ++e)
+        for (int e = 0; e < ptmax; ++e)
             for (int j = 0; j < 2; ++j) {
                 const int k = 2 * i + j;
-                const float v = k < Lx && e < n[k] ? H[(int)(((long)(k + d.rm) * Mx) % Lx) * 21 + off[k] + e] : 0.0f;
+                const float v = k < Lx && e < n[k] ? H[(int)(((long)(k + d.rm) * Mx) % Lx) * Tx + off[k] + e] : 0.0f;
                 fprintf(f, "%s%af", e || j ? ", " : "", (double)v);
             }
         fprintf(f, "}, \\\n");
@@ -178,7 +189,8 @@ int main(int argc, char **argv)
         fprintf(f, "}, \\\n");
     }
     fprintf(f, "}\n");
-    return emit_up(f) || emit_offsets(f, "U2", 44100, 96000, 320, 147) || emit_ratio(f, "32", 3, 2) || emit_ratio(f, "23", 2, 3) || emit_ratio(f, "12", 1, 2) ||
+    return emit_up(f) || emit_offsets(f, "U2", 44100, 96000, 320, 147) ||
+                   emit_offsets_t(f, "D2", 96000, 44100, 147, 320, 46, 43, 44) || emit_ratio(f, "32", 3, 2) || emit_ratio(f, "23", 2, 3) || emit_ratio(f, "12", 1, 2) ||
                    emit_ratio(f, "21", 2, 1) || emit_ratio(f, "31", 3, 1) || fclose(f)
                ? 1
                : 0;
