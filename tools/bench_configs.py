@@ -58,18 +58,83 @@ EQ5 = [(xm.XM_EQ_LOWSHELF, 100.0, 3.0, 0.7), (xm.XM_EQ_PEAKING, 400.0, -2.0, 1.0
        (xm.XM_EQ_HIGHSHELF, 10000.0, 4.0, 0.7)]
 
 
+_SAMPLER = None   # (process, file) of the clock sampler (start_sampler)
+_LAST_WINDOW = None   # wall-clock window of the last timed loop (time.time())
+
+
+def start_sampler():
+    """A child process that never touches HIP polls rocm-smi's current clocks
+    every ~0.3 s into a file (started before any device work: the box refuses
+    an exec from a GPU-initialised process, and rocm-smi re-execs its
+    interpreter).  report() attaches the clocks sampled during each line's
+    timed loop."""
+    global _SAMPLER
+    import subprocess
+    import tempfile
+    f = tempfile.NamedTemporaryFile(prefix="xm_clk_", suffix=".jsonl", delete=False)
+    f.close()
+    code = ("import json,subprocess,time,sys\n"
+            "while True:\n"
+            "    t=time.time()\n"
+            "    try:\n"
+            "        r=subprocess.run(['rocm-smi','--showclocks','--json'],capture_output=True,text=True,timeout=10)\n"
+            "        d=json.loads(r.stdout) if r.stdout.strip().startswith('{') else {}\n"
+            "    except Exception:\n"
+            "        d={}\n"
+            "    c=next((v for v in d.values() if isinstance(v,dict)),{})\n"
+            "    open(sys.argv[1],'a').write(json.dumps({'t':(t+time.time())/2,**{k.split()[0]:v for k,v in c.items() if 'speed' in k}})+'\\n')\n"
+            "    time.sleep(0.3)\n")
+    try:
+        p = subprocess.Popen([sys.executable, "-c", code, f.name], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        _SAMPLER = (p, f.name)
+    except Exception:  # pragma: no cover - box dependent
+        _SAMPLER = None
+
+
+def stop_sampler():
+    if _SAMPLER:
+        _SAMPLER[0].kill()
+        try:
+            os.unlink(_SAMPLER[1])
+        except OSError:
+            pass
+
+
+def clocks_during(window):
+    """Median of each clock rocm-smi reported inside `window` (wall seconds)."""
+    if not _SAMPLER or not window:
+        return None
+    rows = []
+    try:
+        for line in open(_SAMPLER[1]):
+            d = json.loads(line)
+            if window[0] <= d.get("t", 0) <= window[1]:
+                rows.append(d)
+    except (OSError, ValueError):
+        return None
+    out = {"samples": len(rows)}
+    for k in ("sclk", "mclk", "fclk", "socclk"):
+        v = sorted(int("".join(ch for ch in str(r[k]) if ch.isdigit()) or 0) for r in rows if k in r)
+        if v:
+            out[k + "_mhz"] = v[len(v) // 2]
+    return out
+
+
 def timed(step, steps, warmup, stream):
+    global _LAST_WINDOW
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    w0 = time.time()
     e0.record(stream)
     for _ in range(steps):
         step()
     e1.record(stream)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
+    _LAST_WINDOW = (w0, time.time())
     return wall * 1e3, e0.elapsed_time(e1) / steps
 
 
@@ -147,6 +212,9 @@ def report(name, workload, samples, alg_bytes, wall_ms, ker_ms, mixer, launches=
                          "frac": round(alg_bytes / (ker_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
     line.update(extra)
     line["box"] = box_props()
+    clk = clocks_during(_LAST_WINDOW)
+    if clk:
+        line["clocks_during"] = clk
     print(json.dumps(line), flush=True)
 
 
@@ -496,9 +564,14 @@ def main():
     if a.no_box or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ):   # under rocprofv3: no rocm-smi
         _BOX = {}
     box_info()   # before any device work (see box_info)
-    for w in a.which:
-        globals()[w](a)
-        torch.cuda.empty_cache()
+    if _BOX:
+        start_sampler()
+    try:
+        for w in a.which:
+            globals()[w](a)
+            torch.cuda.empty_cache()
+    finally:
+        stop_sampler()
 
 
 if __name__ == "__main__":
