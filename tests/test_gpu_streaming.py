@@ -301,3 +301,63 @@ def test_stream_device_direct_bulk(xm, gpu, ntr):
     assert got == F
     assert fast >= 2, fast
     assert bits_equal(yd.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("pattern", ["big_ragged", "sp_edges", "one_block"])
+@pytest.mark.parametrize("ntr", [8, 3, 12])
+def test_stream_fused_window_path_44_to_48(xm, gpu, pattern, ntr):
+    """44.1k->48k stereo streams (round 5): the super-period-aligned bulk of a
+    release runs on the fused UP kernel as a window job (input at the window
+    frame 147*ob/160 of the first aligned output, 32 real lead-in frames, SP
+    origins alternating parity), the head on the generic kernel; any split
+    equals the whole-signal call bit for bit."""
+    N = 44100 + 77
+    x = np.stack([np.stack([O.gen_f32(SEED, 6400 + 16 * b + t, 2, N) for t in range(ntr)]) for b in range(2)])
+    ramps = (RAMPS8 * 2)[:ntr]
+    m = xm.Mixer(44100, 48000, 2, "f32")
+    m.set_tracks(ramps)
+    want = m.process(x)
+    sizes = {"big_ragged": _blocks(N, [7001, 1, 0, 12345, 147 * 30 + 1, 3]),
+             "sp_edges": _blocks(N, [147 * 5, 147 * 20 + 32, 147 * 7 - 1, 147 * 40]),
+             "one_block": [N]}[pattern]
+    m.stream_begin(2)
+    outs, p, fast = [], 0, 0
+    for n in sizes:
+        outs.append(m.stream_push(x[:, :, p:p + n]))
+        fast += m.timing().fast_launches
+        p += n
+    outs.append(m.stream_flush())
+    fast += m.timing().fast_launches
+    assert fast >= 1, "the fused kernel never ran"
+    assert bits_equal(np.concatenate(outs, axis=1), want)
+
+
+@pytest.mark.parametrize("ntr", [8, 5])
+def test_stream_device_direct_bulk_44_to_48(xm, gpu, ntr):
+    """Device-memory pushes of a 44.1k->48k stream: each large block's aligned
+    bulk on the fused UP kernel straight from the caller's block."""
+    import torch
+    B, N = 3, 44100 + 77
+    x = np.stack([np.stack([O.gen_f32(SEED, 6500 + 16 * b + t, 2, N) for t in range(ntr)]) for b in range(B)])
+    ramps = (RAMPS8 * 2)[:ntr]
+    h = xm.Mixer(44100, 48000, 2, "f32")
+    h.set_tracks(ramps)
+    want = h.process(x)
+    F = h.out_frames(N)
+    m = xm.Mixer(44100, 48000, 2, "f32", mem="device")
+    m.set_tracks(ramps)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    m.stream_begin(B)
+    got, p, fast = 0, 0, 0
+    for n in _blocks(N, [12001, 5, 700, 20000, 3]):
+        blk = xd[:, :, p:p + n].contiguous()
+        got += m.stream_push_strided(blk.data_ptr(), n * 2, ntr * n * 2, n, yd[:, got:].data_ptr(), F * 2, F - got)
+        fast += m.timing().fast_launches
+        p += n
+        del blk
+    got += m.stream_flush_strided(yd[:, got:].data_ptr(), F * 2, F - got)
+    assert got == F
+    assert fast >= 2, fast
+    assert bits_equal(yd.cpu().numpy(), want)

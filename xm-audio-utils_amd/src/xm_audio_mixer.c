@@ -1098,10 +1098,19 @@ size_t xm_audio_mixer_stream_out_frames(const XmAudioMixer *m, size_t frames_in,
  * (job->window; the window keeps them, st_step step 3).  On success *j is cut
  * to the outputs before ob_al for the generic kernel; when the fused kernel
  * does not take the job, *j is left whole. */
+/* The ratios whose fused kernel takes stream windows: 147/160 (48k -> 44.1k)
+ * and 160/147 (44.1k -> 48k, round 5); a super-period is one period, L
+ * outputs from M input frames, so window jobs start on multiples of L. */
+static int st_fused_ratio(const XmAudioMixer *m)
+{
+    const int64_t L = m->table.d.L, M = m->table.d.M;
+    return m->table.fast && ((L == 147 && M == 160) || (L == 160 && M == 147));
+}
+
 static int st_fast_part(XmAudioMixer *m, XmhMixJob *j, int64_t R, const char *win, size_t fb, int *launches)
 {
     const int64_t L = m->table.d.L, M = m->table.d.M;
-    if (L != 147 || M != 160 || !m->table.fast || j->io_flags) return XM_OK;   /* out_conv 1: the kernel's s16 epilogue */
+    if (!st_fused_ratio(m) || j->io_flags) return XM_OK;   /* out_conv 1: the kernel's s16 epilogue */
     const int64_t ob = j->out_base, oe = ob + j->frames_out;
     const int64_t ob_al = (ob + L - 1) / L * L, a0 = ob_al / L * M;
     if (oe - ob_al < 4 * L || a0 >= R || (a0 > 0 && a0 - 32 < m->st_w0)) return XM_OK;   /* too small to pay */
@@ -1137,8 +1146,7 @@ static int st_fast_part(XmAudioMixer *m, XmhMixJob *j, int64_t R, const char *wi
 static int64_t st_direct_cut(const XmAudioMixer *m, int64_t B0, int64_t R, int64_t mend, int flush)
 {
     const int64_t L = m->table.d.L, M = m->table.d.M;
-    if (flush || m->cfg.mem_kind != XM_MEM_DEVICE || L != 147 || M != 160 || !m->table.fast || io_flags(m))
-        return -1;
+    if (flush || m->cfg.mem_kind != XM_MEM_DEVICE || !st_fused_ratio(m) || io_flags(m)) return -1;
     int64_t ob_al = (m->st_out + L - 1) / L * L;
     const int64_t q = (B0 + 32 + M - 1) / M;   /* first SP whose input frame a0 = q*M has its lead-in in the block */
     if (q * L > ob_al) ob_al = q * L;
@@ -1181,7 +1189,8 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
      * frames [B0, a0 + 16) (the last head output reads up to a0 + 10) */
     const int64_t B0 = m->st_recv;
     const int64_t ob_dir = nout ? st_direct_cut(m, B0, R, mend, flush) : -1;
-    const size_t n_app = ob_dir >= 0 ? (size_t)(ob_dir / 147 * 160 + 16 - B0) : n;
+    const int64_t Ld = m->table.d.L, Md = m->table.d.M;
+    const size_t n_app = ob_dir >= 0 ? (size_t)(ob_dir / Ld * Md + 16 - B0) : n;
     /* 1) append the block (or the head's part of it) to the window */
     const size_t keep = (size_t)(m->st_recv - m->st_w0);
     if (keep + n_app > m->st_cap) {
@@ -1238,7 +1247,7 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
             /* the bulk [ob_dir, mend) on the fused kernel, straight from the
              * caller's block: window job at input frame a0, its 32 lead-in
              * frames real samples, ramps shifted by ob_dir */
-            const int64_t a0 = ob_dir / 147 * 160;
+            const int64_t a0 = ob_dir / Ld * Md;
             XmhGain g[XM_MAX_TRACKS];
             for (int t = 0; t < m->n_tracks; ++t) {
                 g[t] = m->gains[t];
@@ -1287,9 +1296,9 @@ static int st_step(XmAudioMixer *m, const void *in, ptrdiff_t ts, ptrdiff_t ms, 
     }
     m->st_out = mend;
     /* 3) drop the frames no later output reads (move the rest to the other buffer) */
-    /* + the fused kernel's 32-frame lead-in (147/160 only: the no-resample
-     * kernels read the window from its first frame) */
-    int64_t w0 = st_first_needed(m, mend) - (m->table.d.L == 147 && m->table.d.M == 160 ? 32 : 0);
+    /* + the fused kernel's 32-frame lead-in (its window ratios only: the
+     * other kernels read the window from its first frame) */
+    int64_t w0 = st_first_needed(m, mend) - (st_fused_ratio(m) ? 32 : 0);
     if (w0 > R) w0 = R;
     if (w0 < m->st_w0) w0 = m->st_w0;
     if (ob_dir >= 0 && w0 >= B0) {
