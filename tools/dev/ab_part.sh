@@ -6,7 +6,7 @@
 #   tools/dev/ab_part.sh <name> "<defines>" [parts, default "1"]
 #   e.g. tools/dev/ab_part.sh lib_nowait "-DXM_AB_NOWAIT" && tools/ab_libs.sh 2 lib lib_nowait
 set -e
-NAME=$1; DEFS=$2; PARTS=${3:-1}
+NAME=${1:?usage: ab_part.sh <name> "<defines>" [parts]}; DEFS=$2; PARTS=${3:-1}
 cd "$(dirname "$0")/../../xm-audio-utils_amd"
 make -s -j8 ARCH=gfx950 >/dev/null
 OBJ=build/obj_$NAME
