@@ -5,7 +5,7 @@ give-back" item 6) on the headline shape.
 Run against the diagnostic build, which stamps s_memtime / s_memrealtime once
 per wave around its whole run (csrc/xm_resample_fast.hip, XM_CLOCK_STAMPS):
 
-    make -C xm-audio-utils_amd ab AB=-DXM_CLOCK_STAMPS ABOUT=lib_clk FAST_PARTS=0
+    tools/dev/ab_part.sh lib_clk -DXM_CLOCK_STAMPS      (part 1, the headline kernels)
     XM_AUDIO_LIB=$PWD/xm-audio-utils_amd/lib_clk/libxm_audio.so python tools/dev/clock_stamp.py
 
 It runs >= --seconds of back-to-back launches (random synthetic PCM), clears
