@@ -375,10 +375,11 @@ def c5(a):
 
 
 def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=False, conv=False,
-           stream=False, oconv=False, far=False):
-    B, ntr = a.mixes, 8
+           stream=False, oconv=False, far=False, ntr=8):
+    B = a.mixes
+    q15, ramps = Q15_RAMPS[:ntr], RAMPS[:ntr]
     m = xm.Mixer(fi, fo, 2, fmt, mem="device", planar=planar, convert_in=conv, convert_out=oconv)
-    m.set_tracks(Q15_RAMPS if fmt == "s16" else RAMPS)
+    m.set_tracks(q15 if fmt == "s16" else ramps)
     F = m.out_frames(N)
     ifmt = "s16" if (fmt == "s16") != conv else "f32"
     isz = 2 if ifmt == "s16" else 4
@@ -444,10 +445,10 @@ def _shape(a, name, fi=48000, fo=44100, fmt="f32", N=480000, ptrs=False, planar=
             if planar:
                 xb = np.ascontiguousarray(xb.reshape(ntr, 2, N).swapaxes(1, 2))
             if fmt == "s16":
-                want = CO.resample_mix_s16(list(xb), Q15_RAMPS, L, M)
+                want = CO.resample_mix_s16(list(xb), q15, L, M)
             else:
                 xf = xb.astype(np.float32) * np.float32(2.0 ** -15) if conv else xb
-                want = CO.resample_mix_f32(list(xf), RAMPS, L, M)
+                want = CO.resample_mix_f32(list(xf), ramps, L, M)
                 if oconv:
                     want = to_s16(want)
             got = (ys[b, :F] if stream else y[b]).cpu().numpy()
@@ -540,6 +541,13 @@ def up(a): _shape(a, "up", fi=44100, fo=48000, N=441000)
 def s16rs(a): _shape(a, "s16rs", fmt="s16")
 def planar(a): _shape(a, "planar", planar=True)
 def conv(a): _shape(a, "conv", conv=True)
+# stereo s16 / planar mixes of fewer than 4 tracks (the same mixes count, so
+# 1/8 .. 3/8 of the input bytes)
+def s16rs1(a): _shape(a, "s16rs1", fmt="s16", ntr=1)
+def s16rs2(a): _shape(a, "s16rs2", fmt="s16", ntr=2)
+def s16rs3(a): _shape(a, "s16rs3", fmt="s16", ntr=3)
+def planar2(a): _shape(a, "planar2", planar=True, ntr=2)
+def conv2(a): _shape(a, "conv2", conv=True, ntr=2)
 def stream(a): _shape(a, "stream", stream=True)
 def oconv(a): _shape(a, "oconv", oconv=True)
 
