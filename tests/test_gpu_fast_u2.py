@@ -3,7 +3,8 @@
 
 A super-period is 147 input frames -> 320 outputs (40 exchange rounds); each
 output runs its own used-tap run (kOffU2 / kPtU2, tools/gen_coefs.c
-emit_offsets), like 44.1k -> 48k.  Every case must run as one fused launch
+emit_offsets), like 44.1k -> 48k.  Round 5 added stereo 1-track rows and
+mono f32 tracks (1-track rows with grouped, transposed stores; mixes of 2-8).  Every case must run as one fused launch
 (fast_launches == 1) and equal the C oracle bit for bit: track counts (phantom
 rows), odd and tiny frame counts, lengths around super-period edges, lanes
 walking several super-periods (XM_FAST_SPLIT_R), padded device strides and
@@ -59,18 +60,6 @@ def test_u2_track_counts_and_lengths(xm, gpu, rates, nt):
         _fast(m)
         ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)
         assert bits_equal(y, ref), N
-
-
-@pytest.mark.parametrize("rates", RATES, ids=IDS)
-def test_u2_one_track_takes_the_generic_kernel(xm, gpu, rates):
-    fi, fo = rates
-    N = 5 * SPI + 11
-    x = _x(4, 1, N, 51000)
-    m = xm.Mixer(fi, fo, 2, "f32")
-    m.set_tracks([dict(gain0=0.75)])
-    y = m.process(x)
-    _fast(m, 0)
-    assert bits_equal(y, CO.batch_resample_mix_f32(x, [dict(gain0=0.75)], L, M, threads=4)[0])
 
 
 @pytest.mark.parametrize("R", [2, 3, 5])
@@ -155,3 +144,90 @@ def test_u2_production_grid_44_96(xm, gpu):
     assert bool(torch.equal(ys[0].view(torch.int32), ys[1].view(torch.int32))), "unwritten outputs"
     del x, ys
     torch.cuda.empty_cache()
+
+
+# ---- round 5: 320/147 mono f32 tracks and stereo 1-track rows ------------------
+
+@pytest.mark.parametrize("rates", RATES, ids=IDS)
+@pytest.mark.parametrize("nt", [1, 3, 8])
+def test_u2_mono(xm, gpu, rates, nt):
+    """Mono f32 tracks at 320/147: 1-track rows (eight clips per wave, the
+    grouped transposed stores DSF) and mixes of 2-8 tracks; odd and short
+    lengths, every output against the C oracle."""
+    fi, fo = rates
+    for N in (20 * SPI + 37, SPI * 16 + 1, SPI + 1, 7):
+        B = 11 if nt == 1 else 3
+        x = np.stack([np.stack([O.gen_f32(SEED, 54000 + N + 16 * b + t, 1, N) for t in range(nt)]) for b in range(B)])
+        ramps = _ramps(nt, _F(N))
+        m = xm.Mixer(fi, fo, 1, "f32")
+        m.set_tracks(ramps)
+        y = m.process(x)
+        _fast(m)
+        assert bits_equal(y, CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)[0]), N
+
+
+@pytest.mark.parametrize("R", [4, 6])
+@pytest.mark.parametrize("nt", [1, 8])
+def test_u2_mono_multi_sp(xm, gpu, monkeypatch, R, nt):
+    """Mono runs of 2 and 3 SPs per plane; clips ending inside a run."""
+    monkeypatch.setenv("XM_FAST_SPLIT_R", str(R))
+    N = SPI * (8 * R * 5 // 2 + 3) + 36
+    B = 11 if nt == 1 else 3
+    x = np.stack([np.stack([O.gen_f32(SEED, 55000 + N + 16 * b + t, 1, N) for t in range(nt)]) for b in range(B)])
+    ramps = _ramps(nt, _F(N))
+    m = xm.Mixer(44100, 96000, 1, "f32")
+    m.set_tracks(ramps)
+    y = m.process(x)
+    _fast(m)
+    assert xm.last_fast_split()[0] == R
+    assert bits_equal(y, CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)[0]), N
+
+
+@pytest.mark.parametrize("rates", RATES, ids=IDS)
+def test_u2_stereo_one_track_rows(xm, gpu, rates):
+    """Stereo 1-track mixes at 320/147 (eight clips per wave: a timeline's
+    per-track resampling, resample-only batches), ramped and unity gain,
+    f32 and s16 output, a ninth clip in a partly filled wave."""
+    fi, fo = rates
+    N, B = 20 * SPI + 37, 9
+    x = _x(B, 1, N, 56000)
+    for ramps in ([dict(gain0=0.75)], _ramps(2, _F(N))[1:2], [dict(gain0=1.0)]):
+        m = xm.Mixer(fi, fo, 2, "f32")
+        m.set_tracks(ramps)
+        y = m.process(x)
+        _fast(m)
+        ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)
+        assert bits_equal(y, ref)
+    c = xm.Mixer(fi, fo, 2, "f32", convert_out=True)
+    c.set_tracks([dict(gain0=0.75)])
+    ys = c.process(x)
+    _fast(c)
+    ref, _ = CO.batch_resample_mix_f32(x, [dict(gain0=0.75)], L, M, threads=4)
+    assert bits_equal(ys, O.sat16(np.rint(ref.astype(np.float32) * np.float32(32768.0))).astype(np.int16))
+
+
+def test_u2_stereo_one_track_multi_sp(xm, gpu, monkeypatch):
+    monkeypatch.setenv("XM_FAST_SPLIT_R", "3")
+    N, B = SPI * (8 * 3 * 5 // 2 + 3) + 37, 11
+    x = _x(B, 1, N, 57000)
+    ramps = _ramps(2, _F(N))[1:2]
+    m = xm.Mixer(44100, 96000, 2, "f32")
+    m.set_tracks(ramps)
+    y = m.process(x)
+    _fast(m)
+    assert xm.last_fast_split()[0] == 3
+    assert bits_equal(y, CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)[0])
+
+
+def test_u2_mono_s16_stays_generic(xm, gpu):
+    """Mono s16 tracks at 320/147 have no fused instantiation: the generic
+    kernel, with the same bits as the oracle."""
+    N, B = 9 * SPI + 3, 3
+    x = np.stack([np.stack([O.gen_s16(SEED, 58000 + 16 * b, 1, N)]) for b in range(B)])
+    q = [dict(gain0_q15=29491)]
+    m = xm.Mixer(44100, 96000, 1, "s16")
+    m.set_tracks(q)
+    y = m.process(x)
+    _fast(m, 0)
+    for b in range(B):
+        assert bits_equal(y[b], CO.resample_mix_s16(list(x[b]), q, L, M)), b
