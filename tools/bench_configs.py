@@ -494,11 +494,11 @@ def _mono(a, name, ntr, B, fi, fo, N):
            parity_check=parity(a, chk))
 
 
-def c1s16(a):
+def c1s16(a, name="c1s16", N=441000):
     """Config 1's own form (mono s16 44.1k -> 48k, unity Q15 gain), batched:
     8192 clips through Mixer(44100, 48000, 1, "s16"): the fused kernel's mono
     s16 (M16) 1-track rows."""
-    B, N = 16 * a.mixes, 441000
+    B = 16 * a.mixes
     m = xm.Mixer(44100, 48000, 1, "s16", mem="device")
     ramps = [dict(gain0_q15=32768)]
     m.set_tracks(ramps)
@@ -517,10 +517,13 @@ def c1s16(a):
             if not beq(y[b].cpu().numpy()[:, None], want):
                 return False
         return True
-    report("c1s16", f"c1s16: {B} mono s16 clips x {N} frames, 44100->48000 s16 (config 1's form)",
+    report(name, f"{name}: {B} mono s16 clips x {N} frames, 44100->48000 s16 (config 1's form)",
            B * N, B * N * 2 + B * F * 2, w, k, m, launches=launches,
            kernel="k_rs147_mix" if fast == launches else ("generic" if not fast else f"{fast}/{launches} fused"),
            parity_check=parity(a, chk))
+
+
+def c1odd(a): c1s16(a, "c1odd", N=441001)   # odd N: every other clip 2 B off a dword (round 5: fused)
 
 
 def r32to48(a): _shape(a, "r32to48", fi=32000, fo=48000, N=320000)
