@@ -1,6 +1,7 @@
 """The fused kernel at L/M = 147/320 (round 5, VERDICT r4 item 5 / SURVEY.md
 §8(f)2): 96k -> 44.1k and 48k -> 22.05k, stereo f32 mixes of 2-8 tracks
-(csrc/xm_resample_d2.hip).
+(csrc/xm_resample_d2.hip), and since round 5 stereo 1-track rows (eight
+clips per wave).
 
 A super-period is 320 input frames -> 147 outputs over a 12-segment window;
 each output runs 43 or 44 used taps in two phases (taps 0..21, then 22.. one
@@ -63,15 +64,57 @@ def test_d2_track_counts_and_lengths(xm, gpu, rates, nt):
 
 
 @pytest.mark.parametrize("rates", RATES, ids=IDS)
-def test_d2_one_track_takes_the_generic_kernel(xm, gpu, rates):
+@pytest.mark.parametrize("N", [5 * SPI + 11, 20 * SPI + 38, SPI - 1, 7])
+def test_d2_one_track_rows(xm, gpu, rates, N):
+    """1-track mixes (round 5): eight clips per wave, each row stored to its own
+    output; a ninth clip in a partly filled wave, ramped and unity gain."""
     fi, fo = rates
-    N = 5 * SPI + 11
-    x = _x(4, 1, N, 51000)
-    m = xm.Mixer(fi, fo, 2, "f32")
-    m.set_tracks([dict(gain0=0.75)])
+    B = 9
+    x = _x(B, 1, N, 51000 + N)
+    for ramps in ([dict(gain0=0.75)], _ramps(2, _F(N))[1:2], [dict(gain0=1.0)]):
+        m = xm.Mixer(fi, fo, 2, "f32")
+        m.set_tracks(ramps)
+        y = m.process(x)
+        _fast(m)
+        assert bits_equal(y, CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)[0]), N
+
+
+@pytest.mark.parametrize("odd", [0, 1])
+def test_d2_one_track_rows_multi_sp_and_tables(xm, gpu, monkeypatch, odd):
+    """1-track rows walking 3 super-periods, clips ending inside a run; a
+    device batch at padded strides; a scattered input pointer table."""
+    import torch
+    monkeypatch.setenv("XM_FAST_SPLIT_R", "3")
+    N, B = SPI * (8 * 3 * 5 // 2 + 3) + 36 + odd, 11
+    x = _x(B, 1, N, 51500 + odd)
+    ramps = _ramps(2, _F(N))[1:2]
+    m = xm.Mixer(96000, 44100, 2, "f32")
+    m.set_tracks(ramps)
     y = m.process(x)
-    _fast(m, 0)
-    assert bits_equal(y, CO.batch_resample_mix_f32(x, [dict(gain0=0.75)], L, M, threads=4)[0])
+    _fast(m)
+    assert xm.last_fast_split()[0] == 3
+    ref, _ = CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)
+    assert bits_equal(y, ref)
+    monkeypatch.delenv("XM_FAST_SPLIT_R")
+    d = xm.Mixer(96000, 44100, 2, "f32", mem="device")
+    d.set_tracks(ramps)
+    F = d.out_frames(N)
+    pad = 12
+    xd = torch.zeros((B, N + pad, 2), dtype=torch.float32, device="cuda")
+    xd[:, :N] = torch.from_numpy(x[:, 0]).cuda()
+    yd = torch.full((B, F + 4, 2), float("nan"), dtype=torch.float32, device="cuda")
+    d.process_strided(xd.data_ptr(), (N + pad) * 2, (N + pad) * 2, yd.data_ptr(), (F + 4) * 2, B, N)
+    torch.cuda.synchronize()
+    _fast(d)
+    assert bits_equal(yd[:, :F].cpu().numpy(), ref)
+    # a scattered input table (evenly spaced outputs: the host passes them
+    # as a stride), on the fused kernel
+    perm = [(b * 5 + 2) % B for b in range(B)]
+    y2 = torch.full((B, F, 2), float("nan"), dtype=torch.float32, device="cuda")
+    d.process_ptrs([xd[b].data_ptr() for b in perm], [y2[b].data_ptr() for b in range(B)], B, N)
+    torch.cuda.synchronize()
+    _fast(d)
+    assert bits_equal(y2.cpu().numpy(), ref[perm])
 
 
 @pytest.mark.parametrize("R", [2, 3, 5])

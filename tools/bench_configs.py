@@ -540,6 +540,7 @@ def m44to96(a): _mono(a, "m44to96", 1, 16 * a.mixes, 44100, 96000, 441000)   # m
 def m24to48(a): _mono(a, "m24to48", 1, 16 * a.mixes, 24000, 48000, 240000)   # mono 1-track rows at 2/1 (round 5)
 def m16to48(a): _mono(a, "m16to48", 1, 16 * a.mixes, 16000, 48000, 160000)   # mono 1-track rows at 3/1 (round 5)
 def s24to48(a): _shape(a, "s24to48", fi=24000, fo=48000, N=240000, ntr=1)   # stereo 1-track rows at 2/1 (round 5)
+def s96to44(a): _shape(a, "s96to44", fi=96000, fo=44100, N=960000, ntr=1)   # stereo 1-track rows at 147/320 (round 5)
 def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)
 def mono1(a): _mono(a, "mono1", 1, 16 * a.mixes, 44100, 48000, 441000)
 def odd(a): _shape(a, "odd", N=480001)

@@ -179,6 +179,13 @@ constexpr bool sched_ok()
     return true;
 }
 static_assert(sched_ok(), "every segment's DMA issued once, within the slot, before its copy; vmcnt fits");
+constexpr bool sched8_ok()   // 1-track rows: 8 stores per store event
+{
+    for (int m = 2; m < NW; ++m)
+        if (8 * vm_after(m) >= 64) return false;
+    return true;
+}
+static_assert(sched8_ok(), "1-track rows: vmcnt fits 8 stores per store event");
 
 struct D2Args {
     const float *in;
@@ -216,9 +223,14 @@ __device__ __forceinline__ float gain_exact(const XmhGain &g, int n)
 
 // ODD: odd frames_in or row bases off the 128-B grid (copy_seg zeroes frame N
 // of a chunk straddling it; the DMA keeps the line two segments share in L2)
-template <bool ODD>
+// SPL (round 5): 1-track rows, eight resample-only clips per wave (a
+// timeline's per-track resampling, batches of clips): row t is clip
+// 8 * mix + t (mix = the wave's pseudo-mix), each stored to its own output
+// (8 stores per store event: vm_after is at most 2 events, 16 < 64)
+template <bool ODD, bool SPL>
 __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
 {
+    constexpr int NS = SPL ? 8 : 1;             // stores per store event
     extern __shared__ __attribute__((aligned(16))) char lds_all[];
     const int wib = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     char *lds = lds_all + wib * LDS_PER_WAVE;
@@ -241,9 +253,12 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
         bool ok[TR];
 #pragma unroll
         for (int t = 0; t < TR; ++t) {
-            ok[t] = t < a.n_tracks && mix < a.n_mix;
+            const int64_t ci = (int64_t)mix * TR + t;   // SPL: this row's clip
+            ok[t] = SPL ? ci < a.n_mix : (t < a.n_tracks && mix < a.n_mix);
             if (a.in_ptrs)
-                p[t] = ok[t] ? (uint64_t)(uintptr_t)a.in_ptrs[(int64_t)mix * a.n_tracks + t] : 0;
+                p[t] = ok[t] ? (uint64_t)(uintptr_t)a.in_ptrs[SPL ? ci : (int64_t)mix * a.n_tracks + t] : 0;
+            else if (SPL)
+                p[t] = (uint64_t)(uintptr_t)((const char *)a.in + ci * a.in_mix_stride * 4);
             else
                 p[t] = (uint64_t)(uintptr_t)((const char *)a.in + (int64_t)mix * a.in_mix_stride * 4 + (int64_t)t * a.track_bytes);
             if (ok[t]) {
@@ -330,13 +345,17 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
     XmhGain gp = a.g[0];
 #pragma unroll
     for (int i = 1; i < TR; ++i)
-        if (tr == i) gp = a.g[i];
+        if (!SPL && tr == i) gp = a.g[i];
     const bool xf = (gp.flags & XMH_GAIN_XFADE_OUT) != 0;
 
-    const bool mix_ok = mix < a.n_mix;
-    char *outb = a.out_ptrs ? (mix_ok ? (char *)a.out_ptrs[mix] : (char *)a.out) : (char *)a.out + (int64_t)mix * a.out_mix_stride * 4;
-    const __amdgpu_buffer_rsrc_t ro =
-        __builtin_amdgcn_make_buffer_rsrc(outb, (short)0, mix_ok ? (int)((uint32_t)a.frames_out * 8u) : 0, 0x00020000);
+    const bool mix_ok = (int64_t)mix * (SPL ? TR : 1) < a.n_mix;
+    // SPL: the clips of this wave at outb + g * clip_bytes (g < n_grp)
+    const int n_grp = SPL ? (int)min((int64_t)TR, a.n_mix - (int64_t)mix * TR) : 1;
+    const uint32_t clip_bytes = SPL ? (uint32_t)a.out_mix_stride * 4u : 0u;
+    char *outb = a.out_ptrs ? (mix_ok ? (char *)a.out_ptrs[mix] : (char *)a.out)
+                            : (char *)a.out + (int64_t)mix * (SPL ? TR : 1) * a.out_mix_stride * 4;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        outb, (short)0, mix_ok ? (int)((uint32_t)(n_grp - 1) * clip_bytes + (uint32_t)a.frames_out * 8u) : 0, 0x00020000);
 
     // track sum: lane' = (slot spo, output kk of the round); rows of every
     // track in track order (phantom rows add +-0)
@@ -345,6 +364,18 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
     auto sum_store = [&](int rp, int qp, bool valid) __attribute__((always_inline)) {
 #pragma unroll
         for (int t2 = 0; t2 < TR; ++t2) pend[t2] = X[kkp * 64 + ((t2 * S + spo + 4 * kkp) & 63)];
+        if constexpr (SPL) {   // each row its own 1-track mix (+ 0), all 8 stores issued (vmcnt)
+            const int kq = qp * G + kkp;
+            const int n = ((task * S + spo) * a.R + rp) * SPO + kq;
+            const bool ok = valid && kq < SPO && n < a.frames_out;
+#pragma unroll
+            for (int g = 0; g < TR; ++g) {
+                const f2 v = pend[g] + f2{0.0f, 0.0f};
+                const uint32_t off = ok ? (uint32_t)g * clip_bytes + (uint32_t)n * 8u : OOB;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), ro, off, 0, 0);
+            }
+            return;
+        }
         f2 v = pend[0];
 #pragma unroll
         for (int k = 1; k < TR; ++k) v = v + pend[k];
@@ -368,7 +399,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
 #pragma unroll
             for (int q = 0; q < PPP; ++q) dma_part(0, 2, i * PPP + q, edge0);
 #pragma unroll
-    for (int i = 0; i < prologue_stores(); ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, ro, OOB, 0, 0);
+    for (int i = 0; i < NS * prologue_stores(); ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, ro, OOB, 0, 0);
 
     f2 acc[4][2];   // phase-A results of the pairs waiting for phase B (pair index % 4)
 #pragma unroll 1
@@ -425,16 +456,16 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
                 // 1. the segments this slot's taps need
 #pragma unroll
                 for (int m = have_before(k) + 1; m <= needc(k); ++m) {
-                    if (m == 2) copy_seg(2, std::integral_constant<int, vm_after(2)>{}, r, edge_cur);
-                    if (m == 3) copy_seg(3, std::integral_constant<int, vm_after(3)>{}, r, edge_cur);
-                    if (m == 4) copy_seg(4, std::integral_constant<int, vm_after(4)>{}, r, edge_cur);
-                    if (m == 5) copy_seg(5, std::integral_constant<int, vm_after(5)>{}, r, edge_cur);
-                    if (m == 6) copy_seg(6, std::integral_constant<int, vm_after(6)>{}, r, edge_cur);
-                    if (m == 7) copy_seg(7, std::integral_constant<int, vm_after(7)>{}, r, edge_cur);
-                    if (m == 8) copy_seg(8, std::integral_constant<int, vm_after(8)>{}, r, edge_cur);
-                    if (m == 9) copy_seg(9, std::integral_constant<int, vm_after(9)>{}, r, edge_cur);
-                    if (m == 10) copy_seg(10, std::integral_constant<int, vm_after(10)>{}, r, edge_cur);
-                    if (m == 11) copy_seg(11, std::integral_constant<int, vm_after(11)>{}, r, edge_cur);
+                    if (m == 2) copy_seg(2, std::integral_constant<int, NS * vm_after(2)>{}, r, edge_cur);
+                    if (m == 3) copy_seg(3, std::integral_constant<int, NS * vm_after(3)>{}, r, edge_cur);
+                    if (m == 4) copy_seg(4, std::integral_constant<int, NS * vm_after(4)>{}, r, edge_cur);
+                    if (m == 5) copy_seg(5, std::integral_constant<int, NS * vm_after(5)>{}, r, edge_cur);
+                    if (m == 6) copy_seg(6, std::integral_constant<int, NS * vm_after(6)>{}, r, edge_cur);
+                    if (m == 7) copy_seg(7, std::integral_constant<int, NS * vm_after(7)>{}, r, edge_cur);
+                    if (m == 8) copy_seg(8, std::integral_constant<int, NS * vm_after(8)>{}, r, edge_cur);
+                    if (m == 9) copy_seg(9, std::integral_constant<int, NS * vm_after(9)>{}, r, edge_cur);
+                    if (m == 10) copy_seg(10, std::integral_constant<int, NS * vm_after(10)>{}, r, edge_cur);
+                    if (m == 11) copy_seg(11, std::integral_constant<int, NS * vm_after(11)>{}, r, edge_cur);
                 }
                 f2 p0, p1, p2, p3;
                 // 2. phase B of outputs k-8, k-7: taps 22.. continuing their chains
@@ -614,16 +645,20 @@ extern "C" int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launch
     const int64_t Nf = j->frames_in;
     if (j->rs.L != L || j->rs.M != M || j->rs.T != T || j->rs.rm != RM || !j->rs.fast) return -1003;
     if (j->channels != 2 || j->fmt != 2 || j->io_flags || j->out_conv || j->window || j->in_base || j->out_base ||
-        j->partial || !j->gains_host || NT < 2 || NT > 8 || Nf <= 0 || Nf >= (1 << 26) || j->n_mix <= 0 ||
+        j->partial || !j->gains_host || NT < 1 || NT > 8 || Nf <= 0 || Nf >= (1 << 26) || j->n_mix <= 0 ||
         (j->in_ptrs && !j->in_ptrs_host))
         return -1003;
+    const bool spl = NT == 1;   // 1-track rows: eight clips per wave
+    if (spl && j->out_ptrs) return -1003;   // per-clip output tables: generic path
+    const int64_t npm = spl ? (j->n_mix + 7) / 8 : j->n_mix;   // the waves' pseudo-mixes
     const int64_t lim = ((int64_t)1 << 31) - (Nf + 32) * 8;
     uintptr_t mis = 0;
     if (j->in_ptrs) {
-        for (int64_t mi = 0; mi < j->n_mix; ++mi) {
+        for (int64_t mi = 0; mi < npm; ++mi) {
             uintptr_t lo = UINTPTR_MAX, hi = 0;
-            for (int t = 0; t < NT; ++t) {
-                const uintptr_t p = (uintptr_t)j->in_ptrs_host[mi * NT + t];
+            for (int t = 0; t < (spl ? 8 : NT); ++t) {
+                if (spl && mi * 8 + t >= j->n_mix) break;
+                const uintptr_t p = (uintptr_t)j->in_ptrs_host[spl ? mi * 8 + t : mi * NT + t];
                 if (p & 3) return -1003;
                 mis |= p;
                 lo = p < lo ? p : lo;
@@ -634,11 +669,15 @@ extern "C" int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launch
     } else {
         const int64_t tb = j->in_track_stride * 4, mb = j->in_mix_stride * 4;
         const int64_t atb = tb < 0 ? -tb : tb;
-        if ((atb & 3) || (mb & 3) || ((uintptr_t)j->in & 3) || atb < Nf * 8) return -1003;
-        if ((int64_t)(NT - 1) * atb >= lim) return -1003;
+        const int64_t amb = mb < 0 ? -mb : mb;
+        if ((atb & 3) || (mb & 3) || ((uintptr_t)j->in & 3) || (!spl && atb < Nf * 8)) return -1003;
+        if (!spl && (int64_t)(NT - 1) * atb >= lim) return -1003;
+        if (spl && j->n_mix > 1 && (amb < Nf * 8 || 7 * amb >= lim)) return -1003;
         mis = (uintptr_t)j->in | (uintptr_t)atb | (uintptr_t)(j->n_mix > 1 ? (mb < 0 ? -mb : mb) : 0);
     }
     if (j->frames_out * 8 >= ((int64_t)1 << 31)) return -1003;
+    if (spl && (j->out_mix_stride < j->frames_out * 2 || 7 * j->out_mix_stride * 4 + j->frames_out * 8 >= ((int64_t)1 << 31)))
+        return -1003;
     D2Args a;
     memset(&a, 0, sizeof a);
     a.in = (const float *)j->in;
@@ -653,17 +692,18 @@ extern "C" int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launch
     a.frames_in = (int32_t)Nf;
     a.frames_out = (int32_t)j->frames_out;
     a.n_sp = (int32_t)((j->frames_out + SPO - 1) / SPO);
-    d2_split(j->n_mix, a.n_sp, &a.R, &a.tasks_per_mix);
+    d2_split(npm, a.n_sp, &a.R, &a.tasks_per_mix);
     for (int i = 0; i < NT; ++i) {
         a.g[i] = j->gains_host[i];
         const int64_t glim = (int64_t)1 << 28;
         a.g[i].start = a.g[i].start < -glim ? -glim : (a.g[i].start > glim ? glim : a.g[i].start);
     }
-    const int64_t waves = (int64_t)j->n_mix * a.tasks_per_mix;
+    const int64_t waves = npm * a.tasks_per_mix;
     const int64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks > 0x7fffffff / WPB) return -1003;
     const bool odd = (Nf & 1) != 0 || (mis & 127) != 0;
-    const void *kern = odd ? (const void *)k_rs_d2_mix<true> : (const void *)k_rs_d2_mix<false>;
+    const void *kern = spl ? (odd ? (const void *)k_rs_d2_mix<true, true> : (const void *)k_rs_d2_mix<false, true>)
+                           : (odd ? (const void *)k_rs_d2_mix<true, false> : (const void *)k_rs_d2_mix<false, false>);
     if (xmg_func_lds(kern, WPB * LDS_PER_WAVE)) return -1001;
     void *kargs[] = {&a};
     if (hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(64 * WPB), kargs, (size_t)(WPB * LDS_PER_WAVE),
