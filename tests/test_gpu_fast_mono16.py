@@ -6,9 +6,10 @@ table ratios, the Q15 mix (s16 out) and s16 tracks into the f32 mix
 (convert_in), 1-track rows (batches of clips) and 2-8-track mixes, ramps
 whose edges fall in either half of a lane's run, short clips and lengths
 around super-period edges, strided device memory and pointer tables.  Every
-dword-aligned case must run on the fused kernel (XmMixerTiming.fast_launches
-== 1); odd frame counts (2-byte aligned tracks) take the generic kernel.  All
-equal the C oracle bit for bit."""
+case must run on the fused kernel (XmMixerTiming.fast_launches == 1): since
+round 5 odd frame counts too (every other clip 2 B off a dword: each row's
+DMA window starts at the dword before its own segment start, and the copy
+shifts by that row's delta).  All equal the C oracle bit for bit."""
 import numpy as np
 import pytest
 
@@ -60,8 +61,7 @@ def _run(xm, rates, x, ramps, fmt="s16", **kw):
     m.set_tracks(ramps)
     y = m.process(x)
     t = m.timing()
-    aligned = x.shape[2] % 2 == 0
-    assert t.n_launches == 1 and t.fast_launches == (1 if aligned else 0), (t.n_launches, t.fast_launches)
+    assert t.n_launches == 1 and t.fast_launches == 1, (t.n_launches, t.fast_launches)
     return y
 
 
@@ -170,6 +170,91 @@ def test_m16_config1_batch_production(xm, gpu):
     for b in (0, B - 1):
         assert bits_equal(y[b].cpu().numpy(), CO.resample_s16(x[b].cpu().numpy(), 160, 147)), b
     # every output written: a second run over another sentinel gives the same bits
+    y1 = y.clone()
+    y.fill_(32767)
+    m.process_strided(x.data_ptr(), N, N, y.data_ptr(), F, B, N)
+    torch.cuda.synchronize()
+    assert bool(torch.equal(y, y1))
+    del x, y, y1
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("N", [9607, 9609, 9608])
+def test_m16_odd_n_device_strides_and_tables(xm, gpu, N):
+    """Odd N in device memory: track strides of an odd number of samples (rows
+    on every 2-B phase), a scattered pointer table with 2-B aligned entries,
+    outputs at odd strides (the exchange-and-store form), both ratios' Q15
+    mix and the f32 mix of s16 tracks."""
+    import torch
+    nt, B = 5, 4
+    x = _xs(B, nt, N, 35000 + N)
+    for rates, fmt in (((44100, 48000), "s16"), ((48000, 44100), "s16"), ((44100, 48000), "f32")):
+        L, M = RATES[rates]
+        F = _F(N, L, M)
+        q = _q15(nt, F) if fmt == "s16" else _f32ramps(nt, F)
+        if fmt == "s16":
+            ref = _ref_s16(x, q, L, M)
+        else:
+            ref, _ = CO.batch_resample_mix_f32(x.astype(np.float32) * np.float32(2.0 ** -15), q, L, M, threads=4)
+        m = xm.Mixer(*rates, 1, fmt, mem="device", convert_in=fmt == "f32")
+        m.set_tracks(q)
+        ts, ms = N + 3, (N + 3) * nt + 1
+        buf = np.zeros(B * ms + 16, np.int16)
+        for b in range(B):
+            for t in range(nt):
+                buf[1 + b * ms + t * ts: 1 + b * ms + t * ts + N] = x[b, t].reshape(-1)
+        xd = torch.from_numpy(buf).cuda()
+        dt = torch.int16 if fmt == "s16" else torch.float32
+        yd = torch.full((B, F + 1), -7, dtype=dt, device="cuda")
+        m.process_strided(xd[1:].data_ptr(), ts, ms, yd.data_ptr(), F + 1, B, N)
+        torch.cuda.synchronize()
+        assert m.timing().fast_launches == 1, (rates, fmt)
+        assert bits_equal(yd.cpu().numpy()[:, :F].reshape(B, F, 1), ref), (rates, fmt)
+        perm = [(3 * t + 2) % nt for t in range(nt)]
+        ins = [xd[1 + b * ms + perm[t] * ts:].data_ptr() for b in range(B) for t in range(nt)]
+        y2 = torch.full((B, F), -7, dtype=dt, device="cuda")
+        outs = [y2[(3 * b + 1) % B].data_ptr() for b in range(B)]
+        m.process_ptrs(ins, outs, B, N)
+        torch.cuda.synchronize()
+        assert m.timing().fast_launches == 1
+        ref2 = _ref_s16(x[:, perm], q, L, M) if fmt == "s16" else \
+            CO.batch_resample_mix_f32(x[:, perm].astype(np.float32) * np.float32(2.0 ** -15), q, L, M, threads=4)[0]
+        got = y2.cpu().numpy()
+        for b in range(B):
+            assert bits_equal(got[(3 * b + 1) % B].reshape(F, 1), ref2[b]), (rates, fmt, b)
+
+
+@pytest.mark.parametrize("nt", [1, 5])
+def test_m16_odd_n_multi_sp(xm, gpu, monkeypatch, nt):
+    """Odd N with lanes walking 2 SP pairs per plane (R = 8): the row delta
+    combines with the SP parity in every segment."""
+    monkeypatch.setenv("XM_FAST_SPLIT_R", "8")
+    N = 147 * (8 * 8 * 5 // 2 + 3) + 37
+    B = 11 if nt == 1 else 3
+    x = _xs(B, nt, N, 36000 + nt)
+    q = _q15(nt, _F(N, 160, 147))
+    y = _run(xm, (44100, 48000), x, q)
+    assert xm.last_fast_split()[0] == 8
+    assert bits_equal(y, _ref_s16(x, q, 160, 147))
+
+
+def test_m16_config1_batch_odd_n(xm, gpu):
+    """Config 1's own form with an odd N, 256 clips, first and last checked,
+    every output written."""
+    import torch
+    B, N = 256, 441001
+    m = xm.Mixer(44100, 48000, 1, "s16", mem="device")
+    m.set_tracks([dict(gain0_q15=32768)])
+    F = m.out_frames(N)
+    x = torch.empty((B, N), dtype=torch.int16, device="cuda")
+    y = torch.full((B, F), -32768, dtype=torch.int16, device="cuda")
+    xm.synth(x.data_ptr(), "s16", SEED, 5, B, 1, N)
+    torch.cuda.synchronize()
+    m.process_strided(x.data_ptr(), N, N, y.data_ptr(), F, B, N)
+    torch.cuda.synchronize()
+    assert m.timing().fast_launches == 1
+    for b in (0, 1, B - 1):
+        assert bits_equal(y[b].cpu().numpy(), CO.resample_s16(x[b].cpu().numpy(), 160, 147)), b
     y1 = y.clone()
     y.fill_(32767)
     m.process_strided(x.data_ptr(), N, N, y.data_ptr(), F, B, N)

@@ -201,8 +201,8 @@ def test_small_mono_f32(xm, gpu, ratio, nt):
 @pytest.mark.parametrize("nt", [1, 5])
 def test_small_mono_s16_q15(xm, gpu, ratio, nt):
     """Mono s16 tracks into the Q15 mix at the small ratios (M16; 2/3 moves
-    every other SP origin by one s16 frame), dword-aligned N on the fused
-    kernel, odd N on the generic one."""
+    every other SP origin by one s16 frame), even and (since round 5) odd N
+    on the fused kernel."""
     fi, fo, L, M, SPI = ratio
     for N in (20 * SPI + 38, 2 * SPI + 2, 20 * SPI + 37):
         B = 11 if nt == 1 else 3
@@ -213,7 +213,7 @@ def test_small_mono_s16_q15(xm, gpu, ratio, nt):
         m.set_tracks(q)
         y = m.process(x)
         t = m.timing()
-        fused = N % 2 == 0 and (L, M, nt) != (3, 2, 1)
+        fused = (L, M, nt) != (3, 2, 1)
         assert t.n_launches == 1 and t.fast_launches == (1 if fused else 0), (N, t.fast_launches)
         ref = np.stack([CO.resample_mix_s16(list(x[b]), q, L, M) for b in range(B)])
         assert bits_equal(y, ref), N
