@@ -77,6 +77,12 @@ def test_d2_one_track_rows(xm, gpu, rates, N):
         y = m.process(x)
         _fast(m)
         assert bits_equal(y, CO.batch_resample_mix_f32(x, ramps, L, M, threads=4)[0]), N
+    c = xm.Mixer(fi, fo, 2, "f32", convert_out=True)   # s16 output
+    c.set_tracks([dict(gain0=0.75)])
+    ys = c.process(x)
+    _fast(c)
+    ref, _ = CO.batch_resample_mix_f32(x, [dict(gain0=0.75)], L, M, threads=4)
+    assert bits_equal(ys, O.sat16(np.rint(ref.astype(np.float32) * np.float32(32768.0))).astype(np.int16))
 
 
 @pytest.mark.parametrize("odd", [0, 1])
@@ -163,10 +169,10 @@ def test_d2_device_strides_tables_s16_out(xm, gpu):
     torch.cuda.synchronize()
     _fast(m)
     assert bits_equal(y[:, :F].cpu().numpy(), ref[perm])
-    c = xm.Mixer(96000, 44100, 2, "f32", convert_out=True)   # s16 output: the generic kernel
+    c = xm.Mixer(96000, 44100, 2, "f32", convert_out=True)   # s16 output (round 5: the fused kernel's epilogue)
     c.set_tracks(ramps)
     ys = c.process(x)
-    _fast(c, 0)
+    _fast(c)
     assert bits_equal(ys, O.sat16(np.rint(ref.astype(np.float32) * np.float32(32768.0))).astype(np.int16))
 
 

@@ -196,7 +196,7 @@ struct D2Args {
     int32_t n_mix, n_tracks;
     int32_t frames_in, frames_out;
     int32_t n_sp, R, tasks_per_mix;
-    int32_t pad;
+    int32_t out_s16;           // 1: the f32 mix stored as s16 = sat16(rint(y * 32768)) (out strides in s16 samples)
     XmhGain g[8];
     const float *const *in_ptrs;
     float *const *out_ptrs;
@@ -349,13 +349,29 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
     const bool xf = (gp.flags & XMH_GAIN_XFADE_OUT) != 0;
 
     const bool mix_ok = (int64_t)mix * (SPL ? TR : 1) < a.n_mix;
+    // output f32 (L, R) pairs, or with out_s16 the s16 pairs of the converted mix
+    const int osz = a.out_s16 ? 2 : 4;          // bytes per output sample
     // SPL: the clips of this wave at outb + g * clip_bytes (g < n_grp)
     const int n_grp = SPL ? (int)min((int64_t)TR, a.n_mix - (int64_t)mix * TR) : 1;
-    const uint32_t clip_bytes = SPL ? (uint32_t)a.out_mix_stride * 4u : 0u;
+    const uint32_t clip_bytes = SPL ? (uint32_t)a.out_mix_stride * (uint32_t)osz : 0u;
     char *outb = a.out_ptrs ? (mix_ok ? (char *)a.out_ptrs[mix] : (char *)a.out)
-                            : (char *)a.out + (int64_t)mix * (SPL ? TR : 1) * a.out_mix_stride * 4;
+                            : (char *)a.out + (int64_t)mix * (SPL ? TR : 1) * a.out_mix_stride * osz;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        outb, (short)0, mix_ok ? (int)((uint32_t)(n_grp - 1) * clip_bytes + (uint32_t)a.frames_out * 8u) : 0, 0x00020000);
+        outb, (short)0, mix_ok ? (int)((uint32_t)(n_grp - 1) * clip_bytes + (uint32_t)a.frames_out * 2u * (uint32_t)osz) : 0,
+        0x00020000);
+    // f32 -> s16 store epilogue (XM_MIXER_OUT_CONVERT; the fused and generic
+    // kernels' xm_round_sat16(y * 32768)), both channels in one dword
+    auto pack_s16 = [](f2 v) __attribute__((always_inline)) {
+        const int32_t l = xm_round_sat16(v.x * 32768.0f), r = xm_round_sat16(v.y * 32768.0f);
+        return ((uint32_t)l & 0xffffu) | ((uint32_t)r << 16);
+    };
+    // one store per (group, store event) either way: the vmcnt counts hold
+    auto store_pair = [&](f2 v, bool ok, uint32_t base, int n) __attribute__((always_inline)) {
+        if (a.out_s16)   // wave-uniform
+            __builtin_amdgcn_raw_buffer_store_b32(pack_s16(v), ro, ok ? base + (uint32_t)n * 4u : OOB, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), ro, ok ? base + (uint32_t)n * 8u : OOB, 0, 0);
+    };
 
     // track sum: lane' = (slot spo, output kk of the round); rows of every
     // track in track order (phantom rows add +-0)
@@ -369,11 +385,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
             const int n = ((task * S + spo) * a.R + rp) * SPO + kq;
             const bool ok = valid && kq < SPO && n < a.frames_out;
 #pragma unroll
-            for (int g = 0; g < TR; ++g) {
-                const f2 v = pend[g] + f2{0.0f, 0.0f};
-                const uint32_t off = ok ? (uint32_t)g * clip_bytes + (uint32_t)n * 8u : OOB;
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), ro, off, 0, 0);
-            }
+            for (int g = 0; g < TR; ++g) store_pair(pend[g] + f2{0.0f, 0.0f}, ok, (uint32_t)g * clip_bytes, n);
             return;
         }
         f2 v = pend[0];
@@ -382,8 +394,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rs_d2_mix(D2Args a)
         v = v + f2{0.0f, 0.0f};   // -0 -> +0 (scipy seeds are +0)
         const int kq = qp * G + kkp;
         const int n = ((task * S + spo) * a.R + rp) * SPO + kq;
-        const uint32_t off = (valid && kq < SPO && n < a.frames_out) ? (uint32_t)n * 8u : OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), ro, off, 0, 0);
+        store_pair(v, valid && kq < SPO && n < a.frames_out, 0u, n);
     };
 
     // prologue: segments 0, 1 in registers; segment 2's parts a previous SP
@@ -644,7 +655,7 @@ extern "C" int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launch
     const int NT = j->n_tracks;
     const int64_t Nf = j->frames_in;
     if (j->rs.L != L || j->rs.M != M || j->rs.T != T || j->rs.rm != RM || !j->rs.fast) return -1003;
-    if (j->channels != 2 || j->fmt != 2 || j->io_flags || j->out_conv || j->window || j->in_base || j->out_base ||
+    if (j->channels != 2 || j->fmt != 2 || j->io_flags || j->out_conv > 1 || j->out_conv < 0 || j->window || j->in_base || j->out_base ||
         j->partial || !j->gains_host || NT < 1 || NT > 8 || Nf <= 0 || Nf >= (1 << 26) || j->n_mix <= 0 ||
         (j->in_ptrs && !j->in_ptrs_host))
         return -1003;
@@ -675,8 +686,9 @@ extern "C" int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launch
         if (spl && j->n_mix > 1 && (amb < Nf * 8 || 7 * amb >= lim)) return -1003;
         mis = (uintptr_t)j->in | (uintptr_t)atb | (uintptr_t)(j->n_mix > 1 ? (mb < 0 ? -mb : mb) : 0);
     }
-    if (j->frames_out * 8 >= ((int64_t)1 << 31)) return -1003;
-    if (spl && (j->out_mix_stride < j->frames_out * 2 || 7 * j->out_mix_stride * 4 + j->frames_out * 8 >= ((int64_t)1 << 31)))
+    const int64_t osz = j->out_conv == 1 ? 2 : 4;   // bytes per output sample (s16 out: XM_MIXER_OUT_CONVERT)
+    if (j->frames_out * 2 * osz >= ((int64_t)1 << 31)) return -1003;
+    if (spl && (j->out_mix_stride < j->frames_out * 2 || 7 * j->out_mix_stride * osz + j->frames_out * 2 * osz >= ((int64_t)1 << 31)))
         return -1003;
     D2Args a;
     memset(&a, 0, sizeof a);
@@ -687,6 +699,7 @@ extern "C" int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launch
     a.track_bytes = j->in_track_stride * 4;
     a.out = (float *)j->out;
     a.out_mix_stride = j->out_mix_stride;
+    a.out_s16 = j->out_conv == 1;
     a.n_mix = j->n_mix;
     a.n_tracks = NT;
     a.frames_in = (int32_t)Nf;
