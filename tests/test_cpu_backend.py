@@ -87,6 +87,9 @@ from test_gpu_streaming import (  # noqa: E402,F401
     test_stream_resample_mix_f32_48_to_44, test_stream_resample_s16_44_to_48_mono, test_stream_mix_s16_same_rate,
     test_stream_mixer_errors, test_effects_stream_chain, test_effects_stream_errors, test_stream_mixed_rates_mid_stream,
 )
+from test_gpu_golden_fused import (  # noqa: E402,F401
+    test_fused_mix_equals_scipy, test_fused_rows_equal_scipy,
+)
 
 
 # ---- the CPU backend through the C ABI itself ----------------------------

@@ -14,7 +14,8 @@ applied to scipy-resampled tracks.  Inputs come from the deterministic
 splitmix64 generator (np_oracle.gen_*), whose first samples are stored too so
 the C / HIP generators are pinned to the same bits.
 
-Usage: python tools/gen_golden.py   (rewrites tests/golden/*.npz + MANIFEST.json)
+Usage: python tools/gen_golden.py           (rewrites tests/golden/*.npz + MANIFEST.json)
+       python tools/gen_golden.py --fused   (only resample_fused.npz and its entry)
 """
 from __future__ import annotations
 
@@ -55,6 +56,103 @@ def bits_equal(a, b):
     a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
     return a.shape == b.shape and a.dtype == b.dtype and np.array_equal(
         a.view(np.uint8), b.view(np.uint8))
+
+
+FUSED_CASES = [
+    # (name, fi, fo, N, C, clip, fmt) -- round 6: scipy outputs at
+    # every ratio a fused kernel serves that had only tables before, with lengths
+    # around the super-period edges (SPI input frames per super-period, below) and
+    # odd N.  fmt "s16": s16 input, s16 output = clip(rint(resample_poly(f32(x)))).
+    # 320/147 (SPI 147): 44.1k -> 96k, 22.05k -> 48k
+    ("u2_44to96_st_146", 44100, 96000, 146, 2, 300, "f32"),
+    ("u2_44to96_st_147", 44100, 96000, 147, 2, 301, "f32"),
+    ("u2_44to96_st_148", 44100, 96000, 148, 2, 302, "f32"),
+    ("u2_44to96_st_1471", 44100, 96000, 1471, 2, 303, "f32"),
+    ("u2_22to48_st_295", 22050, 48000, 295, 2, 304, "f32"),
+    ("u2_22to48_mono_147", 22050, 48000, 147, 1, 305, "f32"),
+    ("u2_22to48_mono_1177", 22050, 48000, 1177, 1, 306, "f32"),
+    # 2/1 (SPI 160): 24k -> 48k, 22.05k -> 44.1k
+    ("x2_24to48_st_159", 24000, 48000, 159, 2, 310, "f32"),
+    ("x2_24to48_st_160", 24000, 48000, 160, 2, 311, "f32"),
+    ("x2_24to48_st_161", 24000, 48000, 161, 2, 312, "f32"),
+    ("x2_24to48_st_1601", 24000, 48000, 1601, 2, 313, "f32"),
+    ("x2_22to44_mono_160", 22050, 44100, 160, 1, 314, "f32"),
+    ("x2_22to44_mono_1283", 22050, 44100, 1283, 1, 315, "f32"),
+    # 3/1 (SPI 160): 16k -> 48k
+    ("x3_16to48_st_161", 16000, 48000, 161, 2, 320, "f32"),
+    ("x3_16to48_st_960", 16000, 48000, 960, 2, 321, "f32"),
+    ("x3_16to48_mono_159", 16000, 48000, 159, 1, 322, "f32"),
+    ("x3_16to48_mono_1121", 16000, 48000, 1121, 1, 323, "f32"),
+    # 1/2 (SPI 160): 96k -> 48k
+    ("d2_96to48_st_160", 96000, 48000, 160, 2, 330, "f32"),
+    ("d2_96to48_st_161", 96000, 48000, 161, 2, 331, "f32"),
+    ("d2_96to48_st_2883", 96000, 48000, 2883, 2, 332, "f32"),
+    ("d2_96to48_mono_319", 96000, 48000, 319, 1, 333, "f32"),
+    ("d2_96to48_mono_3201", 96000, 48000, 3201, 1, 334, "f32"),
+    # 2/3 (SPI 159): 48k -> 32k
+    ("t23_48to32_st_158", 48000, 32000, 158, 2, 340, "f32"),
+    ("t23_48to32_st_159", 48000, 32000, 159, 2, 341, "f32"),
+    ("t23_48to32_st_160", 48000, 32000, 160, 2, 342, "f32"),
+    ("t23_48to32_st_2545", 48000, 32000, 2545, 2, 343, "f32"),
+    ("t23_48to32_mono_1591", 48000, 32000, 1591, 1, 344, "f32"),
+    # 3/2 (SPI 160): 32k -> 48k stereo
+    ("t32_32to48_st_160", 32000, 48000, 160, 2, 350, "f32"),
+    ("t32_32to48_st_1763", 32000, 48000, 1763, 2, 351, "f32"),
+    # 147/320 (SPI 320): 96k -> 44.1k, mono and stereo
+    ("d2x_96to44_mono_319", 96000, 44100, 319, 1, 360, "f32"),
+    ("d2x_96to44_mono_320", 96000, 44100, 320, 1, 361, "f32"),
+    ("d2x_96to44_mono_3201", 96000, 44100, 3201, 1, 362, "f32"),
+    ("d2x_96to44_st_321", 96000, 44100, 321, 2, 363, "f32"),
+    ("d2x_96to44_st_2561", 96000, 44100, 2561, 2, 364, "f32"),
+    # 160/147 and 147/160 mono s16 at odd N (config 1's form, BASELINE.json:7)
+    ("s16_44to48_mono_147", 44100, 48000, 147, 1, 370, "s16"),
+    ("s16_44to48_mono_1471", 44100, 48000, 1471, 1, 371, "s16"),
+    ("s16_44to48_mono_4411", 44100, 48000, 4411, 1, 372, "s16"),
+    ("s16_44to48_mono_14701", 44100, 48000, 14701, 1, 373, "s16"),
+    ("s16_48to44_mono_161", 48000, 44100, 161, 1, 374, "s16"),
+    ("s16_48to44_mono_3201", 48000, 44100, 3201, 1, 375, "s16"),
+    ("s16_44to48_st_1471", 44100, 48000, 1471, 2, 376, "s16"),
+]
+
+
+def fused_vectors():
+    """resample_fused.npz: scipy resample_poly outputs at the fused kernels' ratios."""
+    out = {}
+    for name, fi, fo, N, C, clip, fmt in FUSED_CASES:
+        L, M = O.reduce_ratio(fi, fo)
+        H, T, rm, _, _ = scipy_table(L, M)
+        if fmt == "f32":
+            x = O.gen_f32(SEED, clip, C, N)
+            y = signal.resample_poly(x, L, M, axis=0).astype(np.float32, copy=False)
+            assert y.dtype == np.float32
+            assert bits_equal(O.resample_f32(x, H, L, M, rm), y), name
+        else:
+            x = O.gen_s16(SEED, clip, C, N)
+            yf = signal.resample_poly(x.astype(np.float32), L, M, axis=0)
+            assert yf.dtype == np.float32
+            y = np.clip(np.rint(yf), -32768, 32767).astype(np.int16)
+            assert bits_equal(O.resample_s16(x, H, L, M, rm), y), name
+        out[f"{name}__y"] = y
+        out[f"{name}__meta"] = np.array([fi, fo, N, C, clip, 16 if fmt == "s16" else 32], np.int64)
+    return out
+
+
+def write_manifest_entry(manifest, f):
+    with open(os.path.join(OUT, f), "rb") as fh:
+        data = fh.read()
+    manifest["files"][f] = {"sha256": hashlib.sha256(data).hexdigest(), "bytes": len(data)}
+
+
+def main_fused():
+    """--fused: (re)write only resample_fused.npz and its MANIFEST entry."""
+    np.savez_compressed(os.path.join(OUT, "resample_fused.npz"), **fused_vectors())
+    path = os.path.join(OUT, "MANIFEST.json")
+    with open(path) as fh:
+        manifest = json.load(fh)
+    write_manifest_entry(manifest, "resample_fused.npz")
+    with open(path, "w") as fh:
+        json.dump(manifest, fh, indent=1, sort_keys=True)
+    print(json.dumps(manifest["files"]["resample_fused.npz"]))
 
 
 def main():
@@ -210,17 +308,18 @@ def main():
                                ).astype(np.int16) for s in s_tr[:4]], ramps_q[:4])
     mix["s16_resample4__y"] = ys16r
     np.savez_compressed(os.path.join(OUT, "mix.npz"), **mix)
+    np.savez_compressed(os.path.join(OUT, "resample_fused.npz"), **fused_vectors())
 
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
-            with open(os.path.join(OUT, f), "rb") as fh:
-                data = fh.read()
-            manifest["files"][f] = {"sha256": hashlib.sha256(data).hexdigest(),
-                                    "bytes": len(data)}
+            write_manifest_entry(manifest, f)
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)
     print(json.dumps(manifest, indent=1))
 
 
 if __name__ == "__main__":
-    main()
+    if "--fused" in sys.argv[1:]:
+        main_fused()
+    else:
+        main()

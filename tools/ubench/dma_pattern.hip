@@ -118,7 +118,6 @@ __global__ __launch_bounds__(512) void k_dma(const char *buf, int layout, int de
     constexpr int SPI = 64 / LPS;            // streams per instruction
     constexpr int SEGP = PIECE / 256;        // segments per piece
     float acc = 0.0f;
-    [[maybe_unused]] float4 regs[16];
     // every step moves 16 KiB (16 instructions): with larger pieces a step
     // covers 64 / SEGP of the streams, in turn
 #pragma unroll 1
@@ -130,11 +129,12 @@ __global__ __launch_bounds__(512) void k_dma(const char *buf, int layout, int de
             const int c = lane % LPS;        // 16-B chunk within the piece
             const uint32_t off = (uint32_t)(stream_addr(layout, w, q, j + c / 16) - lo) + (uint32_t)(c % 16) * 16u;
             const uint32_t m0 = ldsb + (uint32_t)d * 1024u;
-            if constexpr (POL == 3) {   // plain loads into registers (no LDS-DMA)
-                float4 v;
-                asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(rs) : "memory");
-                regs[d] = v;
-            } else if constexpr (POL == 0)
+            // (POL 3, plain loads into VGPRs by inline asm, was removed: the asm
+            // result carried no vmcnt dependence, so a register was reused before
+            // its load landed and the kernel faulted (illegal address, round 6).
+            // VGPR-load forms are measured by tools/ubench/hbm_ceiling.hip with
+            // the compiler's buffer-load builtin.)
+            if constexpr (POL == 0)
                 asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds" ::"s"(m0), "v"(off), "s"(rs) : "memory", "m0");
             else if constexpr (POL == 1)
                 asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m0), "v"(off), "s"(rs) : "memory", "m0");
@@ -173,10 +173,6 @@ __global__ __launch_bounds__(512) void k_dma(const char *buf, int layout, int de
             acc += t.x;
         }
         acc += *(const float *)(slot + lane * 16);
-        if constexpr (POL == 3) {
-#pragma unroll
-            for (int d = 0; d < 16; ++d) acc += regs[d].x;
-        }
         for (int i = 0; i < delay; ++i) __builtin_amdgcn_s_sleep(8);
     }
     if (acc == 1234.5f) sink[0] = 1;
@@ -201,13 +197,29 @@ int main(int argc, char **argv)
     auto run = [&](auto kern, const char *name, int layout, int delay) {
         hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 20480);
         kern<<<256, 512, 8 * 20480>>>(buf, layout, delay, sink, obuf);
-        hipDeviceSynchronize();
+        // every launch checked: a variant that fails prints FAILED, never the
+        // previous line's time (round 5's VGPR-load line did)
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            printf("%-10s layout %d delay %3d: FAILED (%s)\n", name, layout, delay, hipGetErrorString(e));
+            fflush(stdout);
+            (void)hipGetLastError();
+            return;
+        }
         float best = 1e9;
         for (int r = 0; r < 3; ++r) {
             hipEventRecord(a);
             kern<<<256, 512, 8 * 20480>>>(buf, layout, delay, sink, obuf);
+            e = hipGetLastError();
             hipEventRecord(b);
-            hipEventSynchronize(b);
+            if (e == hipSuccess) e = hipEventSynchronize(b);
+            if (e != hipSuccess) {
+                printf("%-10s layout %d delay %3d: FAILED (%s)\n", name, layout, delay, hipGetErrorString(e));
+                fflush(stdout);
+                (void)hipGetLastError();
+                return;
+            }
             float ms;
             hipEventElapsedTime(&ms, a, b);
             best = ms < best ? ms : best;
@@ -224,6 +236,15 @@ int main(int argc, char **argv)
         run(k_dma<256, 0, 1, 14>, "b64 sc1 nt", 0, 0);
         run(k_dma<256, 0, 1, 15>, "b64 sc0 sc1 nt", 0, 0);
         run(k_dma<256, 2, 1, 0>, "sc1 loads + b64 def", 0, 0);
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'q') {   // the product's stores beside other read geometries
+        run(k_dma<256, 0, 1, 0>, "p256 + b64", 0, 0);
+        run(k_dma<512, 0, 1, 0>, "p512 + b64", 0, 0);
+        run(k_dma<1024, 0, 1, 0>, "p1024 + b64", 0, 0);
+        run(k_dma<1024, 0, 1, 0>, "p1024 + b64", 3, 0);
+        for (int layout = 1; layout < 4; ++layout) run(k_dma<256, 0, 1, 0>, "p256 + b64", layout, 0);
+        run(k_dma<256, 0, 1, 8>, "coalesced + 1K stores", 2, 0);
         return 0;
     }
     if (argc > 1 && argv[1][0] == 's') {   // output store forms beside the stream
@@ -243,8 +264,6 @@ int main(int argc, char **argv)
         run(k_dma<256, 0, 1, 8>, "1K contiguous", 0, 0);
         run(k_dma<256, 0, 1, 9>, "b64 small footprint", 0, 0);
         run(k_dma<256, 0, 1, 10>, "b64 1K footprint", 0, 0);
-        run(k_dma<256, 3, 0, 0>, "VGPR loads, no stores", 0, 0);
-        run(k_dma<256, 3, 1, 0>, "VGPR loads + b64 stores", 0, 0);
         run(k_dma<256, 0, 0, 0>, "coalesced, no stores", 2, 0);
         run(k_dma<256, 0, 1, 0>, "coalesced + b64 stores", 2, 0);
         run(k_dma<256, 0, 1, 8>, "coalesced + 1K stores", 2, 0);
