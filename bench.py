@@ -112,6 +112,8 @@ def parse(argv=None):
     ap.add_argument("--frames", type=int, default=480000, help="input frames per track (10 s @ 48 kHz)")
     ap.add_argument("--mixes5", type=int, default=512, help="config 5: mixes (all devices)")
     ap.add_argument("--tracks5", type=int, default=64, help="config 5: tracks per mix (all devices)")
+    ap.add_argument("--span-chunks", type=int, default=0,
+                    help="config 5: exchange chunks overlapped with the partials (0: automatic, up to 4)")
     ap.add_argument("--cpu-mixes", type=int, default=48, help="mixes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU-baseline sample")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)   # the baseline's child process
@@ -459,6 +461,7 @@ def c5_check(xs_host_mix, ys_host_mix, ramps):
 
 
 def c5_line(args, *, n_gpus, shards, B, ntr, N, value, ms_per_step, ok, mode, parallelism):
+    from xmaudio import dist as xd
     per = ntr // shards
     dev_bytes = B * per * N * 2 * 2 + (B // shards) * N * 2 * 2   # this device's tracks once + its mixes once
     achieved = dev_bytes / (ms_per_step * 1e-3) / 1e9
@@ -471,7 +474,8 @@ def c5_line(args, *, n_gpus, shards, B, ntr, N, value, ms_per_step, ok, mode, pa
         "config": {"workload": f"{ntr}-track s16 Q15 gain-ramp/crossfade mixdown, {B} mixes x 10 s stereo 48 kHz, "
                                f"tracks spread over {shards} shard(s): int32 partials -> one exchange -> saturate",
                    "mixes": B, "tracks": ntr, "tracks_per_shard": per, "frames": N, "channels": 2,
-                   "shards": shards, "launch": mode, "parallelism": parallelism},
+                   "shards": shards, "launch": mode, "parallelism": parallelism,
+                   "exchange_chunks": xd.span_chunks(args.span_chunks, B // shards) if shards > 1 else 0},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "alg_bytes_per_device_step": dev_bytes, "xgmi_bytes_per_device_step": xgmi,
@@ -498,6 +502,7 @@ def run_c5_local(args, devs):
     ramps = RAMPS64[:ntr]
     m = xm.Mixer(48000, 48000, 2, "s16", mem="device", devices=devs)
     m.set_tracks(ramps)
+    m.set_span_chunks(args.span_chunks)
     xs, ys = [], []
     for d, dev in enumerate(devs):
         with torch.cuda.device(dev):
@@ -530,8 +535,8 @@ def run_c5_local(args, devs):
                 ok &= c5_check(xm_, ys[d][b].cpu().numpy(), ramps)
     distinct = len(set(devs)) == n
     par = (f"{n} shards, tracks of every mix split over devices {devs}; exchange: "
-           + ("in-library RCCL ncclReduceScatter(int32) over xGMI" if distinct
-              else "device copies (a device repeats) + ordered int32 sum"))
+           + ("in-library RCCL ncclReduceScatter(int32) over xGMI, in chunks overlapped with the partials"
+              if distinct else "device copies (a device repeats) + ordered int32 sum, chunk by chunk"))
     print(json.dumps(c5_line(args, n_gpus=len(set(devs)), shards=n, B=B, ntr=ntr, N=N,
                              value=B * ntr * N * 2 / (elapsed / args.steps) / 1e6,
                              ms_per_step=elapsed / args.steps * 1e3, ok=ok, mode="one process",
@@ -560,12 +565,12 @@ def run_c5_ranked(args):
     xm.synth(x.data_ptr(), "s16", SEED, rk.rank * B * per, B * per, 2, N, dev, s.cuda_stream)
     y = torch.empty((B // rk.world, N, 2), dtype=torch.int16, device="cuda")
     for _ in range(args.warmup):
-        xd.mix_spanning_s16(rk, m, x, out=y)
+        xd.mix_spanning_s16(rk, m, x, out=y, chunks=args.span_chunks)
     torch.cuda.synchronize()
     xd.barrier(rk)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        xd.mix_spanning_s16(rk, m, x, out=y)
+        xd.mix_spanning_s16(rk, m, x, out=y, chunks=args.span_chunks)
     torch.cuda.synchronize()
     xd.barrier(rk)
     elapsed = xd.max_over_ranks(rk, time.perf_counter() - t0, device="cuda")
@@ -590,7 +595,8 @@ def run_c5_ranked(args):
             ok &= c5_check(np.concatenate(mine), y[b].cpu().numpy(), ramps)
         ok = xd.min_over_ranks(rk, ok, device="cuda")
     if rk.rank == 0:
-        par = f"{rk.world} ranks, one process per GPU; exchange: torch.distributed reduce_scatter_tensor (RCCL)"
+        par = (f"{rk.world} ranks, one process per GPU; exchange: torch.distributed reduce_scatter_tensor (RCCL), "
+               "asynchronous, in chunks overlapped with the partials")
         print(json.dumps(c5_line(args, n_gpus=rk.world, shards=rk.world, B=B, ntr=ntr, N=N,
                                  value=B * ntr * N * 2 / (elapsed / args.steps) / 1e6,
                                  ms_per_step=elapsed / args.steps * 1e3, ok=ok, mode="torchrun",

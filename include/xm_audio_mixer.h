@@ -215,6 +215,15 @@ XM_API int xm_audio_mixer_mix_spanning_s16(XmAudioMixer *m, const void *const *i
                                            ptrdiff_t in_mix_stride, void *const *out, ptrdiff_t out_mix_stride,
                                            size_t batch, size_t frames_in);
 
+/* Config 5's exchange in chunks (build-owned, round 6): the mixes each device
+ * owns are cut into `chunks` groups; the partials of group k+1 compute while
+ * group k's reduce-scatter crosses xGMI on a stream of its own, so only the
+ * last group's exchange is exposed.  chunks = 0 (the default): up to 4; the
+ * count used is the largest one not above the asked count that divides
+ * batch/n.  Every count gives the same bits (int32 sums are exact in any
+ * order).  XM_EINVAL outside [0, 64]. */
+XM_API int xm_audio_mixer_set_span_chunks(XmAudioMixer *m, int chunks);
+
 /* ---- streaming (build-owned) ----------------------
  * `batch` mixes whose tracks arrive in blocks.  stream_begin() starts them at
  * input frame 0; every stream_push() appends the next frames_in frames of

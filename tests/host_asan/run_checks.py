@@ -259,18 +259,23 @@ def main():
     check("xm_effects_create(n_devices=2) / (3 -> NULL)", bool(hc) and not hz and xm._lib.xm_effects_n_devices(hc) == 2)
     xm._lib.xm_effects_freep(ctypes.byref(ctypes.c_void_p(hc)))
 
-    q64 = s16_tracks(4, 64, 240, base=300)
     ramps64 = (Q15 * 8)[:64]
-    want64 = CO.batch_mix_s16(q64, ramps64)[0]
+    # chunks 0 = automatic (K = 4, 2, 2, 1 for these owned blocks), 1 = one
+    # exchange, 3 = the largest divisor <= 3 (K = 3 for [0]'s 12 mixes)
+    q12 = s16_tracks(12, 64, 240, base=300)
+    want12 = CO.batch_mix_s16(q12, ramps64)[0]
     for devs in ([0], [0, 1], [0, 0], [0, 1, 0, 1]):
-        n = len(devs)
-        sp = xm.Mixer(48000, 48000, 2, "s16", mem="device", devices=devs)
-        sp.set_tracks(ramps64)
-        per = 64 // n
-        ins = [np.ascontiguousarray(q64[:, d * per:(d + 1) * per]) for d in range(n)]
-        outs = [np.zeros((4 // n, 240, 2), np.int16) for _ in range(n)]
-        sp.mix_spanning_s16([a.ctypes.data for a in ins], 480, per * 480, [o.ctypes.data for o in outs], 480, 4, 240)
-        check(f"mix_spanning_s16 {devs}", beq(np.concatenate(outs), want64))
+        for chunks in (0, 1, 3):
+            n = len(devs)
+            sp = xm.Mixer(48000, 48000, 2, "s16", mem="device", devices=devs)
+            sp.set_tracks(ramps64)
+            sp.set_span_chunks(chunks)
+            per = 64 // n
+            ins = [np.ascontiguousarray(q12[:, d * per:(d + 1) * per]) for d in range(n)]
+            outs = [np.zeros((12 // n, 240, 2), np.int16) for _ in range(n)]
+            sp.mix_spanning_s16([a.ctypes.data for a in ins], 480, per * 480, [o.ctypes.data for o in outs], 480, 12,
+                                240)
+            check(f"mix_spanning_s16 {devs} chunks {chunks}", beq(np.concatenate(outs), want12))
 
     # the CPU backend (n_devices = 0 / XM_DEVICE_CPU) under the sanitizers:
     # the resampler's staged blocks, windows, pointer tables, effects and

@@ -10,6 +10,7 @@ import socket
 import sys
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 from conftest import ROOT
@@ -136,7 +137,7 @@ class _OracleMixer:
             o[b * oms: b * oms + S] = O.sat16(p[b * pms: b * pms + S].astype(np.int64))
 
 
-def _worker5(rank, world, port, q):
+def _worker5(rank, world, port, q, chunks=1):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     for p in (os.path.join(ROOT, "xm-audio-utils_amd"), os.path.join(ROOT, "oracle"), ROOT):
@@ -149,24 +150,28 @@ def _worker5(rank, world, port, q):
     per = NT5 // world
     mine = range(per * rank, per * (rank + 1))        # this rank's tracks of every mix
     x = torch.from_numpy(np.stack([np.stack([_tracks5(b)[t] for t in mine]) for b in range(B5)]))
-    y = xd.mix_spanning_s16(rk, _OracleMixer([RAMPS5[t] for t in mine]), x)
+    y = xd.mix_spanning_s16(rk, _OracleMixer([RAMPS5[t] for t in mine]), x, chunks=chunks)
     first, n = xd.owned_mixes(rk, B5)
     assert y.shape == (n, F5, 2)
     xd.finish(rk)
     q.put((rank, first, y.numpy()))
 
 
-def test_two_rank_spanning_mixdown_equals_full_mix():
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_two_rank_spanning_mixdown_equals_full_mix(chunks):
     """Config 5 exchange on CPU: each rank holds half of the 64 tracks of every
-    mix, forms the int32 Q15 partial, the partials meet in reduce_partials (one
-    reduce-scatter, RCCL on GPUs and gloo here) and the owner saturates: every
+    mix, forms the int32 Q15 partial, the partials meet in reduce-scatters
+    (RCCL on GPUs, gloo here; chunks = 2: two asynchronous reduce-scatters,
+    each overlapping the next chunk's partials) and the owner saturates: every
     mix equals the one-process 64-track mix bit for bit, saturation included."""
     import np_oracle as O
+    from xmaudio import dist as xd
+    assert xd.span_chunks(chunks, B5 // 2) == chunks
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker5, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker5, args=(r, world, port, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]

@@ -25,6 +25,10 @@ int xmg_launch_mix_placed(const XmhMixJob *j, void *stream, int *n_launches);
 int xmg_launch_finish_s16(const int32_t *parts, int n_parts, int64_t part_stride, int64_t part_mix_stride,
                           int16_t *out, int64_t out_mix_stride, int64_t batch, int64_t samples, void *stream);
 int xmg_fast_table_check(const float *H, int L, int M, int T);                   /* xm_resample_fast.hip */
+/* the fused kernels' grid split (R super-periods per lane, tasks per mix for
+ * S lanes per track row) and the XM_FAST_SPLIT_R test override (0: none) */
+void xmg_pick_split(int64_t n_mix, int n_sp, int S, int *R_out, int *tpm_out);
+int xmg_forced_split_r(void);
 /* 147/320 (96k -> 44.1k): xm_resample_d2.hip; -1003 when the job is not its shape */
 int xmg_launch_mix_d2(const XmhMixJob *j, void *stream, int *n_launches, int *R_out, int *tpm_out);
 int xmg_d2_table_check(const float *H, int L, int M, int T);

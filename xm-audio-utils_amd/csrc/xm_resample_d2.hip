@@ -621,32 +621,16 @@ extern "C" int xmg_d2_table_check(const float *H, int Lr, int Mr, int Tr)
     return 0;
 }
 
-// SPs per lane and tasks per mix (pick_split of csrc/xm_resample_fast.hip)
+// SPs per lane and tasks per mix: the fused kernel's split (xmg_pick_split,
+// csrc/xm_resample_fast.hip; 8 waves per CU here too) and its test override
 static void d2_split(int64_t n_mix, int n_sp, int *R_out, int *tpm_out)
 {
     const int S = 8;
-    const int64_t slots = (int64_t)xmg_cu_count() * WAVES_PER_CU;
-    const int max_tpm = (n_sp + S - 1) / S;
-    int bestR = (n_sp + S - 1) / S, bestT = 1;
-    double best = 1e300;
-    for (int tpm = 1; tpm <= max_tpm && tpm <= 4096; ++tpm) {
-        const int R = (n_sp + S * tpm - 1) / (S * tpm);
-        if (tpm > 1 && (n_sp + S * R - 1) / (S * R) != tpm) continue;
-        const int64_t waves = n_mix * tpm;
-        const double cost = (double)((waves + slots - 1) / slots) * (R + 1);
-        if (cost < best) {
-            best = cost;
-            bestR = R;
-            bestT = tpm;
-        }
+    xmg_pick_split(n_mix, n_sp, S, R_out, tpm_out);
+    if (const int fR = xmg_forced_split_r()) {
+        *R_out = fR;
+        *tpm_out = (n_sp + S * fR - 1) / (S * fR);
     }
-    const char *e = getenv("XM_FAST_SPLIT_R");   // test knob (xm_resample_fast.hip forced_R)
-    if (e && atoi(e) > 0 && atoi(e) <= 4096) {
-        bestR = atoi(e);
-        bestT = (n_sp + S * bestR - 1) / (S * bestR);
-    }
-    *R_out = bestR;
-    *tpm_out = bestT;
 }
 
 // -1003: not this kernel's job (the caller tries the others); R, tpm: the split

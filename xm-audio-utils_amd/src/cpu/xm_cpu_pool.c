@@ -7,10 +7,15 @@
  * handed out one at a time from an atomic counter, so uneven items balance.
  * One parallel region runs at a time; a region started while another runs
  * (another handle on another thread, or a nested call) runs on its caller.
- * Fork-safe: a child of fork() has none of the parent's workers, so a
- * pthread_atfork handler resets the pool's locks there and the child's first
- * parallel region starts its own workers (Python multiprocessing's fork
- * start method after a CPU-backend call in the parent).
+ * Fork-safe: a child of fork() has none of the parent's workers, so the
+ * child's first parallel region starts its own workers (Python
+ * multiprocessing's fork start method after a CPU-backend call in the
+ * parent).  pthread_atfork handlers, registered when the library loads, take
+ * the region and worker locks around fork(): a fork() waits for a region (or
+ * the pool's initialisation, which runs under the region lock) that another
+ * thread is inside, and the child starts with both locks fresh.  Calling
+ * fork() from inside a parallel region's item function is unsupported (it
+ * would wait for its own region).
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -23,10 +28,9 @@
 #define XMC_MAX_THREADS 512
 
 static struct {
-    pthread_once_t once;
+    _Atomic int ready;            /* 1: sized and workers started (cleared in a forked child) */
     int n;                        /* threads including the caller */
-    int want;                     /* threads asked for (XM_CPU_THREADS or the affinity mask) */
-    int spawn;                    /* 1: workers still to be started (first use, or a forked child) */
+    int want;                     /* threads asked for (XM_CPU_THREADS or the affinity mask); 0: not sized yet */
     pthread_mutex_t mu, region;
     pthread_cond_t go, done;
     unsigned long gen;
@@ -35,7 +39,7 @@ static struct {
     void *ctx;
     int64_t n_items;
     _Atomic int64_t next;
-} P = {PTHREAD_ONCE_INIT, 0, 0, 0, PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER,
+} P = {0, 0, 0, PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER,
        PTHREAD_COND_INITIALIZER, 0, 0, NULL, NULL, 0, 0};
 
 static void drain(XmcItemFn fn, void *ctx, int64_t n)
@@ -66,7 +70,7 @@ static void *worker(void *arg)
     return NULL;
 }
 
-/* start the workers (P.mu held or no worker running yet) */
+/* start the workers (P.region held, no worker running) */
 static void spawn_workers(void)
 {
     P.n = 1;
@@ -80,11 +84,23 @@ static void spawn_workers(void)
         if (rc) break;   /* fewer threads than asked: still correct */
         P.n++;
     }
-    P.spawn = 0;
 }
 
-/* fork() child: only the forking thread exists; the parent's workers, and any
- * lock one of them held, are gone */
+/* fork(): no region and no initialisation in flight while the address space
+ * is copied; the parent carries on, the child has only the forking thread
+ * (the parent's workers are gone) and fresh locks */
+static void atfork_prepare(void)
+{
+    pthread_mutex_lock(&P.region);
+    pthread_mutex_lock(&P.mu);
+}
+
+static void atfork_parent(void)
+{
+    pthread_mutex_unlock(&P.mu);
+    pthread_mutex_unlock(&P.region);
+}
+
 static void atfork_child(void)
 {
     pthread_mutex_init(&P.mu, NULL);
@@ -94,47 +110,49 @@ static void atfork_child(void)
     P.gen = 0;
     P.busy = 0;
     P.n = 1;
-    P.spawn = 1;
+    atomic_store(&P.ready, 0);   /* the first region starts the child's own workers */
 }
 
-static void init_pool(void)
+__attribute__((constructor)) static void register_atfork(void)
 {
-    int n = 0;
-    const char *e = getenv("XM_CPU_THREADS");
-    if (e && atoi(e) > 0) {
-        n = atoi(e);
-    } else {
-        cpu_set_t set;
-        if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
-    }
-    if (n < 1) n = 1;
-    if (n > XMC_MAX_THREADS) n = XMC_MAX_THREADS;
-    P.want = n;
-    spawn_workers();
-    pthread_atfork(NULL, NULL, atfork_child);
+    pthread_atfork(atfork_prepare, atfork_parent, atfork_child);
 }
 
-/* a forked child's first use starts its own workers (under the region lock) */
-static void respawn_if_forked(void)
+/* size the pool on first use and start its workers (again in a forked child) */
+static void ensure_pool(void)
 {
-    if (!P.spawn) return;
+    if (atomic_load(&P.ready)) return;
     pthread_mutex_lock(&P.region);
-    if (P.spawn) spawn_workers();
+    if (!atomic_load(&P.ready)) {
+        if (!P.want) {
+            int n = 0;
+            const char *e = getenv("XM_CPU_THREADS");
+            if (e && atoi(e) > 0) {
+                n = atoi(e);
+            } else {
+                cpu_set_t set;
+                if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+            }
+            if (n < 1) n = 1;
+            if (n > XMC_MAX_THREADS) n = XMC_MAX_THREADS;
+            P.want = n;
+        }
+        spawn_workers();
+        atomic_store(&P.ready, 1);
+    }
     pthread_mutex_unlock(&P.region);
 }
 
 int xmc_threads(void)
 {
-    pthread_once(&P.once, init_pool);
-    respawn_if_forked();
+    ensure_pool();
     return P.n;
 }
 
 int xmc_parallel(int64_t n, XmcItemFn fn, void *ctx)
 {
     if (n <= 0) return 0;
-    pthread_once(&P.once, init_pool);
-    respawn_if_forked();
+    ensure_pool();
     if (P.n == 1 || n == 1 || pthread_mutex_trylock(&P.region) != 0) {
         for (int64_t i = 0; i < n; ++i) fn(ctx, i);   /* serial: one item, one thread, or the pool is busy */
         return 0;

@@ -54,6 +54,7 @@ struct XmAudioMixer {
     int64_t *place_dev;            /* [XM_MAX_TRACKS][2] */
     XmhGain *unity_dev;            /* one unity-gain descriptor */
     XmMulti *multi;                /* multi-device handle: every call dispatches here */
+    int span_chunks;               /* config 5: exchange chunks (0: automatic) */
     /* the time-block pipeline of resample -> biquad cascades -> mix (config 4,
      * run_fx_pipelined): the CU-masked biquad, resample and mix streams (split
      * fx_k of every 32 CUs), events per block, the biquad states and the
@@ -65,6 +66,11 @@ struct XmAudioMixer {
     size_t fx_state_cap;
     void **fx_dtab, **fx_htab;
     size_t fx_tab_cap;
+    /* the sequential effects path (run_with_effects): device pointer tables of
+     * the track list and the two scratch sets, grown on demand and kept (a
+     * hipFree per call would synchronise the whole device) */
+    void *fx_seq_tab;
+    size_t fx_seq_tab_cap;
 };
 
 void *xm_mixer_stream(const XmAudioMixer *m) { return m->stream; }
@@ -99,6 +105,17 @@ static int out_bytes(const XmAudioMixer *m)
 {
     const int conv = (m->cfg.flags & XM_MIXER_OUT_CONVERT) != 0;
     return fmt_bytes(conv ? (m->cfg.sample_fmt == XM_FMT_S16 ? XM_FMT_F32 : XM_FMT_S16) : m->cfg.sample_fmt);
+}
+
+static const XmhGain k_unity_desc = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
+
+/* the handle's device copy of one unity-gain descriptor, made on first use */
+static int ensure_unity(XmAudioMixer *m)
+{
+    if (m->unity_dev) return XM_OK;
+    int rc = xmh_malloc((void **)&m->unity_dev, sizeof k_unity_desc);
+    if (!rc) rc = xmh_memcpy_h2d(m->unity_dev, &k_unity_desc, sizeof k_unity_desc, m->stream);
+    return rc;
 }
 
 static int grow(void **p, size_t *cap, size_t need)
@@ -254,6 +271,7 @@ void xm_audio_mixer_freep(XmAudioMixer **pm)
     xmh_free(m->fx_state);
     xmh_free(m->fx_dtab);
     xmh_host_free(m->fx_htab);
+    xmh_free(m->fx_seq_tab);
     for (int i = 0; i < 6; ++i) xmh_event_destroy(m->ev[i]);
     xmh_stream_destroy(m->own_stream);
     free(m);
@@ -512,10 +530,13 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     int K = 0;
     bs[0] = 0;
     for (int k = 1; k <= XM_FX_BLOCKS; ++k) {
-        /* whole groups of 8 super-periods (1176 outputs): every block starts on
-         * a 64-B boundary of the f32 stereo scratch rows (1176 x 8 B = 147 x 64 B),
-         * so the window jobs' whole-segment stores (k_rs147_mix SEG, sc1)
-         * write each 64-B line once, and the biquad and mix read whole lines */
+        /* whole groups of 8 super-periods (1176 outputs).  For stereo (C == 2)
+         * every block then starts on a 64-B boundary of the f32 scratch rows
+         * (1176 x 8 B = 147 x 64 B), so the window jobs' whole-segment stores
+         * (k_rs147_mix SEG, sc1) write each 64-B line once and the biquad and
+         * mix read whole lines.  Mono rows (1176 x 4 B = 4704 B) start odd
+         * blocks 32 B off that grid: correct (stores are range-checked per
+         * output), only the line-once property is stereo's */
         int64_t b = k == XM_FX_BLOCKS ? F : (F * cut32[k] / 32 + 1175) / 1176 * 1176;
         b = b > F ? F : b;
         if (b > bs[K]) bs[++K] = b;
@@ -538,11 +559,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     for (int a = 0; !rc && a < 3; ++a)
         for (int k = 0; !rc && k < XM_FX_BLOCKS; ++k)
             if (!m->fx_ev[a][k]) rc = xmh_event_create(&m->fx_ev[a][k]);
-    if (!rc && !m->unity_dev) {
-        static const XmhGain ug = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
-        rc = xmh_malloc((void **)&m->unity_dev, sizeof ug);
-        if (!rc) rc = xmh_memcpy_h2d(m->unity_dev, &ug, sizeof ug, m->stream);
-    }
+    if (!rc) rc = ensure_unity(m);
     /* biquad states [stage][clip][section][z0, z1][channel], zero at clip start */
     const size_t st_floats = (size_t)ns * ntot * (size_t)max_sos * 2u * (size_t)C;
     if (!rc && m->fx_state_cap < st_floats) {
@@ -572,7 +589,6 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
     for (int i = 0; !rc && i < 3; ++i) rc = xmh_stream_wait(m->fx_s[i], m->fx_ev[2][0]);
     if (!rc) rc = xmh_memcpy_h2d(m->fx_dtab, m->fx_htab, ntab * sizeof(void *), sb);
     if (!rc) rc = xmh_memset(m->fx_state, 0, st_floats * sizeof(float), sb);
-    static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
     const int64_t elem = (int64_t)in_bytes(m);
     for (int k = 0; !rc && k < K; ++k) {
         const int64_t o0 = bs[k], bl = bs[k + 1] - bs[k];
@@ -584,7 +600,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
         r.in_mix_stride = j0->in_track_stride;   /* track i of the flat list */
         r.in_track_stride = 0;
         r.gains = m->unity_dev;
-        r.gains_host = &unity_gain;
+        r.gains_host = &k_unity_desc;
         r.unity = 1;
         r.out_conv = 0;
         r.out = scratch + (size_t)o0 * C;
@@ -674,24 +690,26 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         return rc;
     }
     /* 1) resample: treat every track as its own 1-track mix (unity gain) */
-    static const XmhGain unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
-    XmhGain *ug = NULL;
-    rc = xmh_malloc((void **)&ug, sizeof unity_gain);
+    rc = ensure_unity(m);
     if (rc) return rc;
-    rc = xmh_memcpy_h2d(ug, &unity_gain, sizeof unity_gain, m->stream);
+    /* device pointer tables, one handle buffer: [0, ntot) the track list (when
+     * the mixes are not ntr tracks apart), [ntot, 3 ntot) the two scratch sets */
+    rc = grow(&m->fx_seq_tab, &m->fx_seq_tab_cap, sizeof(void *) * ntot * 3);
+    if (rc) return rc;
+    void **dtab = (void **)m->fx_seq_tab;
     XmhMixJob r = *j0;
     r.out_conv = 0;   /* tracks stay f32 in scratch; the final mix converts */
     r.io_flags = j0->io_flags & ~XMH_IO_OUT_PLANAR;   /* scratch is interleaved */
     r.n_tracks = 1;
     r.n_mix = (int32_t)ntot;
-    r.gains = ug;
-    r.gains_host = &unity_gain;
+    r.gains = m->unity_dev;
+    r.gains_host = &k_unity_desc;
     r.unity = 1;
     r.out = scratch;
     r.out_ptrs = NULL;
     r.out_mix_stride = (int64_t)per_track;
     const void **tp = NULL;   /* host table of the track pointers (irregular strides) */
-    void **dtp = NULL;        /* its device copy: a buffer of its own (m->d_ptrs may hold j0's output table) */
+    void **dtp = dtab;        /* its device copy: not m->d_ptrs, which may hold j0's output table */
     if (j0->in_ptrs) {
         r.in_ptrs = j0->in_ptrs;   /* same mix-major order */
     } else if (j0->n_mix == 1 || j0->in_mix_stride == (int64_t)ntr * j0->in_track_stride) {
@@ -706,17 +724,15 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
             tp[i] = (const char *)j0->in +
                     ((int64_t)(i / (size_t)ntr) * j0->in_mix_stride + (int64_t)(i % (size_t)ntr) * j0->in_track_stride) *
                         elem;
-        if (!rc) rc = xmh_malloc((void **)&dtp, sizeof(void *) * ntot);
         if (!rc) rc = xmh_memcpy_h2d(dtp, tp, sizeof(void *) * ntot, m->stream);
         r.in_ptrs = (const void *const *)dtp;
         r.in_ptrs_host = tp;
     }
     if (!rc) rc = xmh_launch_mix(&r, m->stream, launches, &m->timing.fast_launches);
     /* 2) effects chain on every track, in insertion order */
-    void **tmp_ptrs = NULL;
+    void **tmp_ptrs = dtab + ntot;
     int cur = 0;   /* 0: tracks in scratch, 1: in scratch2 */
     if (!rc && ns > 0) {
-        rc = xmh_malloc((void **)&tmp_ptrs, sizeof(void *) * ntot * 2);
         void **hp = malloc(sizeof(void *) * ntot * 2);
         if (!hp) rc = XM_ENOMEM;
         if (!rc) {
@@ -765,10 +781,7 @@ static int run_with_effects(XmAudioMixer *m, const XmhMixJob *j0, int *launches)
         x.io_flags = j0->io_flags & XMH_IO_OUT_PLANAR;   /* reads the f32 interleaved scratch */
         rc = xmh_launch_mix(&x, m->stream, launches, &m->timing.fast_launches);
     }
-    xmh_stream_sync(m->stream);
-    xmh_free(tmp_ptrs);
-    xmh_free(ug);
-    xmh_free(dtp);
+    xmh_stream_sync(m->stream);   /* tp and the tables are read by the launches */
     free(tp);
     return rc;
 }
@@ -1354,7 +1367,6 @@ int xm_audio_mixer_stream_flush(XmAudioMixer *m, void *out, ptrdiff_t out_mix_st
  * per-track resample bit for bit: 0 + 1*r == r, and a Q15 unity term is the
  * sample itself), then placed at its output-frame offset and mixed with the
  * gains evaluated at the mix's output frame. */
-static const XmhGain k_unity_gain = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
 
 static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrackPlacement *place,
                            void *const *out, size_t batch, size_t out_frames)
@@ -1362,11 +1374,7 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
     const int ntr = m->n_tracks, C = m->cfg.channels, elem = fmt_bytes(m->cfg.sample_fmt);
     int rc = XM_OK, launches = 0;
     if (!m->place_dev && (rc = xmh_malloc((void **)&m->place_dev, sizeof(int64_t) * 2 * XM_MAX_TRACKS))) return rc;
-    if (!m->unity_dev) {
-        static const XmhGain ug = {1.0f, 1.0f, 0.0f, 32768, 32768, 0, 0, 0, 0};
-        if ((rc = xmh_malloc((void **)&m->unity_dev, sizeof ug))) return rc;
-        if ((rc = xmh_memcpy_h2d(m->unity_dev, &ug, sizeof ug, m->stream))) return rc;
-    }
+    if ((rc = ensure_unity(m))) return rc;
     /* resampled lengths and scratch offsets */
     int64_t pl[2 * XM_MAX_TRACKS];
     size_t off[XM_MAX_TRACKS], scratch = 0;
@@ -1412,7 +1420,7 @@ static int timeline_device(XmAudioMixer *m, const void *const *in, const XmTrack
         j.out = (char *)m->d_fx + off[tr];
         j.out_mix_stride = pl[2 * tr + 1] * C;
         j.gains = m->unity_dev;
-        j.gains_host = &k_unity_gain;
+        j.gains_host = &k_unity_desc;
         j.unity = 1;
         j.rs.L = t->d.L;
         j.rs.M = t->d.M;
@@ -1504,6 +1512,13 @@ int xm_audio_mixer_process_sharded(XmAudioMixer *m, const void *const *in, ptrdi
                                           frames_in);
 }
 
+int xm_audio_mixer_set_span_chunks(XmAudioMixer *m, int chunks)
+{
+    if (!m || chunks < 0 || chunks > 64) return XM_EINVAL;
+    m->span_chunks = chunks;
+    return XM_OK;
+}
+
 int xm_audio_mixer_mix_spanning_s16(XmAudioMixer *m, const void *const *in, ptrdiff_t in_track_stride,
                                     ptrdiff_t in_mix_stride, void *const *out, ptrdiff_t out_mix_stride, size_t batch,
                                     size_t frames_in)
@@ -1512,7 +1527,7 @@ int xm_audio_mixer_mix_spanning_s16(XmAudioMixer *m, const void *const *in, ptrd
     if (m->fx || m->mixed_rates) return XM_ENOSYS;
     if (m->multi)
         return xm_multi_mix_spanning_s16(m->multi, in, in_track_stride, in_mix_stride, out, out_mix_stride, batch,
-                                         frames_in);
+                                         frames_in, m->span_chunks);
     /* one device holds every track: no exchange, the plain mix */
     if (m->cfg.sample_fmt != XM_FMT_S16 || m->cfg.mem_kind != XM_MEM_DEVICE || (m->cfg.flags & XM_MIXER_OUT_CONVERT) ||
         io_flags(m))

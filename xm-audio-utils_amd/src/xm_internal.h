@@ -77,7 +77,7 @@ size_t xm_multi_stream_out_frames(const XmMulti *mu, size_t frames_in, int flush
 int  xm_multi_stream_step(XmMulti *mu, const void *in, ptrdiff_t ts, ptrdiff_t ms, size_t n, void *out,
                           ptrdiff_t os, size_t out_cap, size_t *frames_out, int flush);
 int  xm_multi_mix_spanning_s16(XmMulti *mu, const void *const *in, ptrdiff_t ts, ptrdiff_t ms, void *const *out,
-                               ptrdiff_t os, size_t batch, size_t frames_in);
+                               ptrdiff_t os, size_t batch, size_t frames_in, int chunks);
 /* the stream a single-device handle launches on (its own or the caller's) */
 void *xm_mixer_stream(const XmAudioMixer *m);
 /* a single-device handle's current track list */

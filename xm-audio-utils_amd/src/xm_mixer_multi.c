@@ -43,6 +43,7 @@ struct XmMulti {
     int comm_ready;
     void *part[XM_MAX_DEVICES], *recv[XM_MAX_DEVICES];
     size_t part_cap[XM_MAX_DEVICES], recv_cap[XM_MAX_DEVICES];
+    void *cstream[XM_MAX_DEVICES];     /* the reduce-scatters' streams, beside the partials' */
 };
 
 /* run task on every device (device d on worker d) and join; the first failing
@@ -125,6 +126,10 @@ void xm_multi_free(XmMulti *mu)
     for (int d = 0; d < mu->n; ++d) {
         if (mu->comm[d]) xmh_comm_destroy(mu->comm[d]);
         xmh_set_device(mu->devs[d]);
+        if (mu->cstream[d]) {
+            xmh_stream_sync(mu->cstream[d]);
+            xmh_stream_destroy(mu->cstream[d]);
+        }
         xmh_free(mu->part[d]);
         xmh_free(mu->recv[d]);
         xm_audio_mixer_freep(&mu->sub[d]);
@@ -382,13 +387,23 @@ int xm_multi_stream_step(XmMulti *mu, const void *in, ptrdiff_t ts, ptrdiff_t ms
     return rc;
 }
 
-/* ---- config 5: tracks spanning devices ----------------------------------- */
+/* ---- config 5: tracks spanning devices -----------------------------------
+ * The owned blocks (device q finishes mixes [q*nb, (q+1)*nb)) are cut into K
+ * chunks of cb = nb/K mixes; chunk k is mixes q*nb + k*cb .. + cb of every
+ * owner q.  Each device writes the int32 partial of chunk k as [n owners][cb
+ * mixes][S] at part + k*n*cb*S, so one reduce-scatter of that region gives
+ * device d the summed partials of its cb mixes of the chunk.  On distinct
+ * devices chunk k's reduce-scatter runs on a stream of its own while chunk
+ * k+1's partials compute: the xGMI exchange hides behind the HBM-bound
+ * partials except for the last chunk's.  int32 sums are
+ * exact in any order, so every K gives the same bits. */
 typedef struct {
     const void *const *in;
     void *const *out;
     ptrdiff_t ts, ms, os;
     size_t batch, frames, fo, S, nb;
-    int phase;   /* 0 partials, 1 exchange by copies + finish, 2 finish after RCCL */
+    size_t K, cb, k;   /* chunks, mixes per owner and chunk, the chunk of this dispatch */
+    int phase;         /* 0 partials of chunk k; 1 its exchange by copies + finish; 2 finish after RCCL */
 } XmSpanArg;
 
 static int grow_on(int dev, void **p, size_t *cap, size_t need)
@@ -408,37 +423,53 @@ static int t_span(XmMulti *mu, int d, void *p)
 {
     const XmSpanArg *a = p;
     XmAudioMixer *s = mu->sub[d];
-    const size_t blk = a->nb * a->S;   /* int32 per owned block */
+    const size_t cblk = a->cb * a->S;   /* int32 per owner in one chunk */
     mu->ran[d] = 1;
     int rc = xmh_set_device(mu->devs[d]);
     if (rc) return rc;
-    if (a->phase == 0) {
+    if (a->phase == 0) {   /* chunk k's partial, owner by owner: [q][cb][S] */
         rc = grow_on(mu->devs[d], &mu->part[d], &mu->part_cap[d], a->batch * a->S * sizeof(int32_t));
-        if (!rc) rc = xm_audio_mixer_process_partial_s16(s, a->in[d], a->ts, a->ms, (int32_t *)mu->part[d],
-                                                         (ptrdiff_t)a->S, a->batch, a->frames);
+        int32_t *dst = (int32_t *)mu->part[d] + a->k * (size_t)mu->n * cblk;
+        for (int q = 0; q < mu->n && !rc; ++q) {
+            const size_t m0 = (size_t)q * a->nb + a->k * a->cb;   /* first mix of owner q in chunk k */
+            rc = xm_audio_mixer_process_partial_s16(s, (const int16_t *)a->in[d] + (ptrdiff_t)m0 * a->ms, a->ts, a->ms,
+                                                    dst + (size_t)q * cblk, (ptrdiff_t)a->S, a->cb, a->frames);
+        }
         return rc;
     }
-    if (a->phase == 1) {   /* block d of every device's partial, then the ordered sum over parts */
-        rc = grow_on(mu->devs[d], &mu->recv[d], &mu->recv_cap[d], (size_t)mu->n * blk * sizeof(int32_t));
+    int16_t *out = (int16_t *)a->out[d];
+    if (a->phase == 1) {   /* owner d's piece of every device's chunk k, then the ordered sum over parts */
+        rc = grow_on(mu->devs[d], &mu->recv[d], &mu->recv_cap[d], (size_t)mu->n * cblk * sizeof(int32_t));
         void *st = xm_mixer_stream(s);
         for (int q = 0; q < mu->n && !rc; ++q)
-            rc = xmh_memcpy_peer((int32_t *)mu->recv[d] + (size_t)q * blk, mu->devs[d],
-                                 (const int32_t *)mu->part[q] + (size_t)d * blk, mu->devs[q], blk * sizeof(int32_t),
-                                 st);
+            rc = xmh_memcpy_peer((int32_t *)mu->recv[d] + (size_t)q * cblk, mu->devs[d],
+                                 (const int32_t *)mu->part[q] + (a->k * (size_t)mu->n + (size_t)d) * cblk, mu->devs[q],
+                                 cblk * sizeof(int32_t), st);
         if (!rc)
-            rc = xm_audio_mixer_finish_s16(s, (const int32_t *)mu->recv[d], mu->n, (ptrdiff_t)blk, (ptrdiff_t)a->S,
-                                           (int16_t *)a->out[d], a->os, a->nb, a->fo);
+            rc = xm_audio_mixer_finish_s16(s, (const int32_t *)mu->recv[d], mu->n, (ptrdiff_t)cblk, (ptrdiff_t)a->S,
+                                           out + (ptrdiff_t)(a->k * a->cb) * a->os, a->os, a->cb, a->fo);
         return rc;
     }
-    /* phase 2: the reduce-scatter already summed block d into recv[d] on this stream */
-    rc = xm_audio_mixer_finish_s16(s, (const int32_t *)mu->recv[d], 1, 0, (ptrdiff_t)a->S, (int16_t *)a->out[d],
-                                   a->os, a->nb, a->fo);
+    /* phase 2: the reduce-scatters summed every chunk of block d into recv[d] ([nb][S], mix order) */
+    rc = xmh_stream_sync(mu->cstream[d]);
+    if (!rc)
+        rc = xm_audio_mixer_finish_s16(s, (const int32_t *)mu->recv[d], 1, 0, (ptrdiff_t)a->S, out, a->os, a->nb,
+                                       a->fo);
     if (!rc) rc = xmh_comm_check(mu->comm[d]);
     return rc;
 }
 
+/* K: the largest count <= the asked one (0: 4) that divides the owned block */
+static size_t span_chunks(int asked, size_t nb)
+{
+    size_t k = asked > 0 ? (size_t)asked : 4;
+    if (k > nb) k = nb;
+    while (k > 1 && nb % k) --k;
+    return k ? k : 1;
+}
+
 int xm_multi_mix_spanning_s16(XmMulti *mu, const void *const *in, ptrdiff_t ts, ptrdiff_t ms, void *const *out,
-                              ptrdiff_t os, size_t batch, size_t frames_in)
+                              ptrdiff_t os, size_t batch, size_t frames_in, int chunks)
 {
     const int n = mu->n;
     if (mu->cfg.sample_fmt != XM_FMT_S16 || mu->cfg.mem_kind != XM_MEM_DEVICE ||
@@ -471,31 +502,55 @@ int xm_multi_mix_spanning_s16(XmMulti *mu, const void *const *in, ptrdiff_t ts, 
     a.fo = xm_resample_out_frames(mu->cfg.in_rate, mu->cfg.out_rate, frames_in);
     a.S = a.fo * (size_t)mu->cfg.channels;
     a.nb = batch / (size_t)n;
+    a.K = span_chunks(chunks, a.nb);
+    a.cb = a.nb / a.K;
     if (a.fo == 0) return XM_OK;
-    int rc = run_all(mu, t_span, &a);   /* 1) partials, joined */
-    if (rc) return rc;
-    if (!mu->distinct) {                /* 2) exchange by device copies + ordered finish */
-        a.phase = 1;
-        return run_all(mu, t_span, &a);
+    int rc = XM_OK;
+    if (!mu->distinct) {   /* a repeated device: per chunk, partials (joined), then copies + ordered finish */
+        for (a.k = 0; a.k < a.K && !rc; ++a.k) {
+            a.phase = 0;
+            rc = run_all(mu, t_span, &a);
+            a.phase = 1;
+            if (!rc) rc = run_all(mu, t_span, &a);
+        }
+        return rc;
     }
-    /* 2) one reduce-scatter over the devices (RCCL over xGMI), issued as one group */
+    /* distinct devices: RCCL over xGMI, chunk k's reduce-scatter (one group
+     * over the devices, on the exchange streams) beside chunk k+1's partials */
     if (!mu->comm_ready) {
         if ((rc = xmh_comm_init_all(mu->comm, n, mu->devs))) return rc;
         mu->comm_ready = 1;
     }
-    for (int d = 0; d < n && !rc; ++d)
+    for (int d = 0; d < n && !rc; ++d) {
         rc = grow_on(mu->devs[d], &mu->recv[d], &mu->recv_cap[d], a.nb * a.S * sizeof(int32_t));
-    if (rc) return rc;
-    if ((rc = xmh_group_start())) return rc;
-    for (int d = 0; d < n; ++d) {
-        int r2 = xmh_set_device(mu->devs[d]);
-        if (!r2)
-            r2 = xmh_reduce_scatter_i32((const int32_t *)mu->part[d], (int32_t *)mu->recv[d], a.nb * a.S, mu->comm[d],
-                                        xm_mixer_stream(mu->sub[d]));
-        if (!rc) rc = r2;
+        if (!rc && !mu->cstream[d] && !(rc = xmh_set_device(mu->devs[d]))) rc = xmh_stream_create(&mu->cstream[d]);
     }
-    int r3 = xmh_group_end();
-    if (rc || r3) return rc ? rc : r3;
-    a.phase = 2;                        /* 3) saturate the owned blocks */
+    if (rc) return rc;
+    const size_t cblk = a.cb * a.S;
+    int queued = 0;
+    for (a.k = 0; a.k < a.K && !rc; ++a.k) {
+        a.phase = 0;
+        rc = run_all(mu, t_span, &a);   /* chunk k's partials on every device, joined */
+        if (rc) break;
+        if ((rc = xmh_group_start())) break;
+        for (int d = 0; d < n; ++d) {
+            int r2 = xmh_set_device(mu->devs[d]);
+            if (!r2)
+                r2 = xmh_reduce_scatter_i32((const int32_t *)mu->part[d] + a.k * (size_t)n * cblk,
+                                            (int32_t *)mu->recv[d] + a.k * cblk, cblk, mu->comm[d], mu->cstream[d]);
+            if (!rc) rc = r2;
+        }
+        const int r3 = xmh_group_end();
+        if (!rc) rc = r3;
+        queued = 1;
+    }
+    if (rc) {   /* leave no exchange in flight */
+        for (int d = 0; queued && d < n; ++d) {
+            xmh_set_device(mu->devs[d]);
+            xmh_stream_sync(mu->cstream[d]);
+        }
+        return rc;
+    }
+    a.phase = 2;   /* saturate the owned blocks once their exchanges landed */
     return run_all(mu, t_span, &a);
 }

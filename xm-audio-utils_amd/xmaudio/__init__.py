@@ -66,7 +66,7 @@ EXPORTED = [
     "xm_audio_mixer_process_timeline",
     "xm_audio_mixer_create_multi", "xm_audio_mixer_n_devices", "xm_audio_mixer_process_sharded",
     "xm_audio_mixer_mix_spanning_s16", "xm_effects_create_multi", "xm_effects_n_devices",
-    "xm_audio_mixer_last_fast_split",
+    "xm_audio_mixer_last_fast_split", "xm_audio_mixer_set_span_chunks",
 ]
 
 
@@ -150,6 +150,7 @@ _sigs = {
     "xm_effects_create_multi": (_vp, [C.POINTER(XmEffectsConfig), C.POINTER(_i), _i, C.POINTER(_i)]),
     "xm_effects_n_devices": (_i, [_vp]),
     "xm_audio_mixer_last_fast_split": (_i, [C.POINTER(_i), C.POINTER(_i)]),
+    "xm_audio_mixer_set_span_chunks": (_i, [_vp, _i]),
 }
 for _n, (_r, _a) in _sigs.items():
     if os.environ.get("XM_AUDIO_LIB") and not hasattr(_lib, _n):
@@ -404,6 +405,10 @@ class Mixer:
         _check(_lib.xm_audio_mixer_process_sharded(self._h, (C.c_void_p * n)(*in_ptrs), in_track_stride,
                                                    in_mix_stride, (C.c_void_p * n)(*out_ptrs), out_mix_stride,
                                                    (C.c_size_t * n)(*batches), frames_in), "process_sharded")
+
+    def set_span_chunks(self, chunks: int):
+        """Config 5: the exchange in `chunks` groups overlapped with the partials (0: automatic)."""
+        _check(_lib.xm_audio_mixer_set_span_chunks(self._h, chunks), "set_span_chunks")
 
     def mix_spanning_s16(self, in_ptrs, in_track_stride: int, in_mix_stride: int, out_ptrs,
                          out_mix_stride: int, batch: int, frames_in: int):

@@ -100,13 +100,50 @@ def finish_block_s16(mixer, blk, channels, out=None):
     return out
 
 
-def mix_spanning_s16(r: Rank, mixer, x, out=None):
+def span_chunks(asked: int, owned: int) -> int:
+    """The largest chunk count <= asked (0: 4) that divides the owned block
+    (xm_audio_mixer_set_span_chunks' rule)."""
+    k = min(asked if asked > 0 else 4, max(owned, 1))
+    while k > 1 and owned % k:
+        k -= 1
+    return max(k, 1)
+
+
+def mix_spanning_s16(r: Rank, mixer, x, out=None, chunks: int = 0):
     """Config 5 on this rank.  x: [batch, tracks_here, frames, C] int16 in HBM,
     this rank's tracks of every mix (mixer.set_tracks holds their ramps).
     Returns [batch/world, out_frames, C] int16: the finished mixes
-    owned_mixes() gives this rank (partial -> reduce_partials -> finish)."""
-    blk = reduce_partials(r, partial_s16(mixer, x))
-    return finish_block_s16(mixer, blk, x.shape[3], out)
+    owned_mixes() gives this rank (partial -> reduce-scatter -> finish).
+
+    The exchange runs in K chunks (span_chunks(chunks, batch/world)): chunk k
+    is mixes q*n + k*cb .. + cb of every owner q (n = batch/world, cb = n/K);
+    its partial is formed owner by owner into a [world*cb, S] buffer and its
+    reduce-scatter is issued asynchronously, so it crosses the links while
+    chunk k+1's partials compute (the in-library form does the same,
+    src/xm_mixer_multi.c).  int32 sums are exact in any order: every K gives
+    the same bits."""
+    if r.world <= 1:
+        return finish_block_s16(mixer, partial_s16(mixer, x), x.shape[3], out)
+    import torch
+    import torch.distributed as dist
+    B, T, F, C = x.shape
+    _, n = owned_mixes(r, B)
+    K = span_chunks(chunks, n)
+    cb = n // K
+    S = mixer.out_frames(F) * C
+    x = x.contiguous()
+    blk = torch.empty((n, S), dtype=torch.int32, device=x.device)
+    pending = []
+    for k in range(K):
+        buf = torch.empty((r.world * cb, S), dtype=torch.int32, device=x.device)
+        for q in range(r.world):
+            m0 = q * n + k * cb
+            mixer.process_partial_strided(x[m0].data_ptr(), F * C, T * F * C, buf[q * cb].data_ptr(), S, cb, F)
+        work = dist.reduce_scatter_tensor(blk[k * cb:(k + 1) * cb], buf, op=dist.ReduceOp.SUM, async_op=True)
+        pending.append((work, buf))
+    for work, _ in pending:
+        work.wait()
+    return finish_block_s16(mixer, blk, C, out)
 
 
 def barrier(r: Rank) -> None:
