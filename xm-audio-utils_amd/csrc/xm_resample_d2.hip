@@ -59,7 +59,7 @@ constexpr int DLY = G;                     // phase B of output k runs at slot k
 constexpr int SLOT_BYTES = 64 * 256;
 constexpr int X_F2 = G * 64;
 constexpr int LDS_PER_WAVE = SLOT_BYTES + X_F2 * 8;   // 20 KiB
-constexpr int WAVES_PER_CU = 8;
+// (8 waves per CU, as the fused kernel: the split is xmg_pick_split's)
 constexpr int WPB = 8;
 constexpr uint32_t OOB = 0x80000000u;
 constexpr int DMA_PARTS = 8;               // a segment's 16 DMA instructions, 2 per part
