@@ -322,6 +322,8 @@ def headline_line(args, *, n_gpus, shards, B, ntr, N, F, value, ms_per_step, ker
                      "launches_per_step": launches},
         "cpu_baseline": cpu,
     }
+    if _BOX:
+        line["box"] = dict(_BOX)
     if ok is not None:
         line["parity_check"] = ok
         line["parity_detail"] = "bit-exact vs oracle/xm_oracle.c: first and last mix of every shard"
@@ -604,11 +606,40 @@ def run_c5_ranked(args):
     xd.finish(rk)
 
 
+_BOX = {}
+
+
+def box_ids():
+    """The GPU's HBM vendor and VBIOS (rocm-smi), read before this process
+    touches the GPU (rocm-smi re-execs its interpreter, which a process whose
+    GPU is initialised may not do); skipped under rocprofv3, whose preload
+    initialises the GPU first.  Box classes differ in memory-side speed
+    (DESIGN §5.3); the line names its box."""
+    if _BOX or any(k.startswith("ROCPROF") for k in os.environ):
+        return _BOX
+    import subprocess
+    for flag, keys in (("--showmemvendor", ("GPU memory vendor",)), ("--showvbios", ("VBIOS version",)),
+                       ("--showserial", ("Serial Number",))):
+        try:
+            r = subprocess.run(["rocm-smi", flag, "--json"], capture_output=True, text=True, timeout=20)
+            d = json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip().startswith("{") else {}
+            for kv in d.values():
+                if isinstance(kv, dict):
+                    for k in keys:
+                        if k in kv:
+                            _BOX[k] = kv[k]
+                    break
+        except Exception:   # pragma: no cover - box dependent
+            pass
+    return _BOX
+
+
 def main(argv=None):
     args = parse(argv)
     if args.cpu_only:
         run_cpu_only(args)
         return
+    box_ids()   # before any device work
     world = int(os.environ.get("WORLD_SIZE", "1"))
     mode, devs = plan(args, world, torch.cuda.device_count())
     if args.config == "c5":

@@ -380,38 +380,24 @@ __global__ __launch_bounds__(128) void k_biquad_pipe(XmhFxJob j)
 //     PL[(i + 1) & 1] -- every chunk has two steps to land;
 //   store (wave 2): the last section's rows O[(i - 1) & 1] (chunk i - ns),
 //     interleaved in registers, to HBM, never waiting for a store;
-//   wave 1: stereo, a second chain wave over the workgroup's other clips
-//     (round 6); mono, it only keeps the barrier count.
+//   wave 1 only keeps the barrier count (the SIMD order 0, 2, 1, 3 puts the
+//     store wave beside the chain wave on the LDS store path).
 // One barrier per step; chunks are 64 frames.  Rows are skewed by 4 floats
 // per row so the 16-B row accesses of a wave are bank-conflict free.
-// Two chain waves (stereo): a workgroup's waves take the SIMDs in the cyclic
-// order 0, 2, 1, 3 from a varying start, so waves 0 and 1 always sit on
-// different SIMDs.  Round 5's form had one chain wave per workgroup and two
-// workgroups per CU: on the 128 CUs config 4's pipeline gives the biquad, two
-// chain waves of different workgroups could meet on one SIMD, and the issue-
-// bound chain (36 cycles per frame at one wave per SIMD) then
-// ran 245 us per 32nd of the clip against 230 us alone (profiles/
-// r4_q_c4_timeline.txt).  One workgroup of two chain waves per CU (93 KB of
-// LDS) holds the same 12 clips on half the CUs with no such collision.
 constexpr int PC_CH = 64;                          // frames per chunk (per channel)
 constexpr int PC_KPW = 12;                         // clips per workgroup at most
 constexpr int PC_OS = 2 * PC_CH + 4;               // floats per lane: O[parity][frame] + skew
 constexpr int PC_RS = PC_CH + 4;                   // floats per planar input row + skew
-constexpr int PC_O0 = 0;                           // O rows (floats), 64 per chain wave
-template <int C>
-struct PcLayout {
-    static constexpr int NCW = C == 2 ? 2 : 1;     // chain waves
-    static constexpr int IN0 = PC_O0 + NCW * 64 * PC_OS;   // inb[chunk & 1][clip]: chunks of PC_CH * C floats
-    static constexpr int PL0 = IN0 + 2 * PC_KPW * PC_CH * 2;   // PL[chunk & 1][clip][ch]: rows of PC_RS floats
-    static constexpr size_t LDS = (size_t)(PL0 + 2 * PC_KPW * 2 * PC_RS) * 4;   // 92,928 B stereo, 59,136 B mono
-    static_assert(IN0 % 4 == 0 && PL0 % 4 == 0, "16-B rows");
-};
-// clips per chain wave and per workgroup (src/xm_audio_mixer.c run_fx_pipelined
-// restates this and the workgroups per CU: 1 stereo, 2 mono)
-__host__ __device__ constexpr int pc_kpc(int ns, int C) { return (16 / ns) * (4 / C) < PC_KPW / (C == 2 ? 2 : 1) ? (16 / ns) * (4 / C) : PC_KPW / (C == 2 ? 2 : 1); }
-static_assert(PcLayout<1>::LDS <= 80 * 1024, "mono: two workgroups per CU");
-static_assert(PcLayout<2>::LDS <= 160 * 1024, "stereo: one workgroup per CU");
-static_assert(PC_OS % 64 == 4 && PC_RS % 64 == 4, "4-float skew per row");
+constexpr int PC_O0 = 0;                           // O rows (floats)
+constexpr int PC_IN0 = PC_O0 + 64 * PC_OS;         // inb[chunk & 1][clip]: chunks of PC_CH * C floats, contiguous
+constexpr int PC_PL0 = PC_IN0 + 2 * PC_KPW * PC_CH * 2;   // PL[chunk & 1][clip][ch]: rows of PC_RS floats
+constexpr size_t PC_LDS = (size_t)(PC_PL0 + 2 * PC_KPW * 2 * PC_RS) * 4;   // 59,136 B
+// two workgroups per CU (src/xm_audio_mixer.c run_fx_pipelined sizes its CU
+// partition for that; 128-frame chunks, 116 KB: bq 7.07 ms against 7.36, but
+// one workgroup per CU)
+static_assert(PC_LDS <= 80 * 1024, "two workgroups per CU");
+static_assert(PC_OS % 64 == 4 && PC_RS % 64 == 4 && PC_IN0 % 4 == 0 && PC_PL0 % 4 == 0,
+              "16-B rows, 4-float skew per row");
 
 // vmcnt(n) for a wave-uniform n <= 12 (the DMA groups of one chunk)
 __device__ __forceinline__ void pc_vm_wait(int n)
@@ -440,7 +426,6 @@ __device__ __forceinline__ void pc_vm_wait(int n)
 template <int C>
 __device__ __forceinline__ void pc_load_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, float *lf)
 {
-    constexpr int PC_IN0 = PcLayout<C>::IN0, PC_PL0 = PcLayout<C>::PL0;
     typedef const __attribute__((address_space(1))) float gcf;
     typedef __attribute__((address_space(3))) void lds_void;
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -529,7 +514,6 @@ template <int C>
 __device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int nclip, int64_t steps, int ns,
                                               float *lf)
 {
-    const int kpc = pc_kpc(ns, C);                 // clips per chain wave
     typedef __attribute__((address_space(1))) float gf;
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef float f2 __attribute__((ext_vector_type(2)));
@@ -551,9 +535,8 @@ __device__ __forceinline__ void pc_store_wave(const XmhFxJob &j, int clip0, int 
         const int k = min(g * CPI + kl, nclip - 1);
         yp[g] = j.out_ptrs[clip0 + k];
         ya[g] = (uint64_t)(uintptr_t)yp[g] + (uint64_t)sg * 16u;
-        const int cw = k / kpc, kl = k % kpc;     // chain wave, clip within it
-        const int ln = ((kl / CPG) * ns + ns - 1) * 4 + (kl % CPG) * C;   // its lane of (clip, last, ch 0)
-        orow[g] = PC_O0 + (cw * 64 + ln) * PC_OS;
+        const int ln = ((k / CPG) * ns + ns - 1) * 4 + (k % CPG) * C;   // the chain lane of (clip, last, ch 0)
+        orow[g] = PC_O0 + ln * PC_OS;
     }
     __syncthreads();
     for (int64_t i = 0; i < steps; ++i) {
@@ -594,11 +577,9 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
     constexpr int CPG = 4 / C;                     // clips per group (a block of 4 lanes)
     extern __shared__ bq_f4 bq_lds[];
     float *lf = (float *)bq_lds;
-    constexpr int NCW = PcLayout<C>::NCW, PC_PL0 = PcLayout<C>::PL0;
     const int ns = j.n_sos;
     const int gpw = 16 / ns;                       // groups per wave
-    const int kpc = pc_kpc(ns, C);                 // clips per chain wave
-    const int kpw = NCW * kpc;                     // clips per workgroup
+    const int kpw = min(gpw * CPG, PC_KPW);        // clips per workgroup
     const int clip0 = blockIdx.x * kpw;
     const int nclip = min(kpw, j.n_clips - clip0);
     const int64_t N = j.frames;
@@ -618,21 +599,20 @@ __global__ __launch_bounds__(256) void k_biquad_pc(XmhFxJob j)
         pc_store_wave<C>(j, clip0, nclip, steps, ns, lf);
         return;
     }
-    if (NCW == 1 && wave == 1) {   // barriers only
+    if (wave == 1) {   // barriers only
         __syncthreads();
         for (int64_t i = 0; i < steps; ++i) __syncthreads();
         return;
     }
-    const int cw = wave;                           // chain wave 0 or 1: clips cw * kpc ..
     const int lane = threadIdx.x & 63;
     const int blk = lane >> 2, r = lane & 3;
     const int grp = blk / ns, s = blk % ns, ci = r / C, ch = r % C;
-    const int kk = cw * kpc + grp * CPG + ci;      // clip within the workgroup
-    const bool valid = blk < gpw * ns && grp * CPG + ci < kpc && kk < nclip;
+    const int kk = grp * CPG + ci;
+    const bool valid = blk < gpw * ns && kk < nclip;
     const int kq = valid ? kk : 0;
     const float *q = j.sos + 6 * (valid ? s : 0);
     const float b0 = q[0], b1 = q[1], b2 = q[2], a1 = q[4], a2 = q[5];
-    const int O_lane = PC_O0 + (cw * 64 + lane) * PC_OS;
+    const int O_lane = PC_O0 + lane * PC_OS;
 
     // ---------------- chain: 6 VALU per frame ---------------------------------
     const float na1 = -a1, na2 = -a2;              // (-a)*o == -(a*o): IEEE negation is exact
@@ -951,12 +931,17 @@ extern "C" int xmg_launch_fx_biquad(const XmhFxJob *j, void *stream)
     if (j->n_sos <= 16) {
         auto pk = j->channels == 2 ? (j->state ? k_biquad_pc<2, true> : k_biquad_pc<2, false>)
                                    : (j->state ? k_biquad_pc<1, true> : k_biquad_pc<1, false>);
-        const int C = j->channels;
-        const int kpw = (C == 2 ? PcLayout<2>::NCW : PcLayout<1>::NCW) * pc_kpc(j->n_sos, C);
-        const size_t lds = C == 2 ? PcLayout<2>::LDS : PcLayout<1>::LDS;
-        if (xmg_func_lds((const void *)pk, (int)lds)) return -1001;   // once per (kernel, device)
+        const int kpw = std::min(16 / j->n_sos * (4 / j->channels), PC_KPW);
+        // dev knob XM_BQ_LDS=bytes: a larger LDS request (>= 81920: one
+        // workgroup per CU) for placement experiments
+        static const int lds_req = [] {
+            const char *e = getenv("XM_BQ_LDS");
+            const int v = e ? atoi(e) : 0;
+            return v > (int)PC_LDS && v <= 160 * 1024 ? v : (int)PC_LDS;
+        }();
+        if (xmg_func_lds((const void *)pk, lds_req)) return -1001;   // once per (kernel, device)
         XmhFxJob jj = *j;
-        hipLaunchKernelGGL(pk, dim3((unsigned)((j->n_clips + kpw - 1) / kpw)), dim3(256), lds,
+        hipLaunchKernelGGL(pk, dim3((unsigned)((j->n_clips + kpw - 1) / kpw)), dim3(256), (size_t)lds_req,
                            (hipStream_t)stream, jj);
         return hipGetLastError() == hipSuccess ? 0 : -1001;
     }

@@ -498,27 +498,32 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
         return XM_ENOSYS;
     if (j0->n_mix > 1 && j0->in_mix_stride != (int64_t)ntr * j0->in_track_stride) return XM_ENOSYS;
     int max_sos = 0;
-    int64_t nwg = 0;   /* biquad workgroups of the largest stage (csrc/xm_fx.hip pc_kpc, PcLayout) */
-    const int ncw = C == 2 ? 2 : 1;   /* chain waves per k_biquad_pc workgroup */
+    int64_t nwg = 0;   /* biquad workgroups of the largest stage (k_biquad_pc: 16 / n groups of 4 / C clips) */
     for (int s = 0; s < ns; ++s) {
         if (st[s].kind != 1 || st[s].n > 16) return XM_ENOSYS;   /* FIR stages: history handling, the three passes */
         max_sos = st[s].n > max_sos ? st[s].n : max_sos;
-        int kpc = 16 / st[s].n * (4 / C);   /* clips per chain wave */
-        kpc = kpc < 12 / ncw ? kpc : 12 / ncw;
-        const int64_t w = ((int64_t)ntot + ncw * kpc - 1) / (ncw * kpc);
+        int kpw = 16 / st[s].n * (4 / C);
+        kpw = kpw < 12 ? kpw : 12;
+        const int64_t w = ((int64_t)ntot + kpw - 1) / kpw;
         nwg = w > nwg ? w : nwg;
     }
-    /* the CU split: the biquad grid resident at once (k_biquad_pc: stereo one
-     * workgroup of two chain waves per CU, 93 KB of LDS; mono two workgroups
-     * of 59 KB), the other CUs for the resample and the mix; k a multiple of
-     * 8 of every 32 CUs, so every XCD gets the same share */
-    const int wgpc = C == 2 ? 1 : 2;
+    /* the CU split: the biquad grid resident at once (two k_biquad_pc
+     * workgroups per CU: 59 KB of LDS each, csrc/xm_fx.hip PC_LDS), the other
+     * CUs for the resample and the mix; k a multiple of 8 of every 32 CUs, so
+     * every XCD gets the same share.  (Round 6 tried one workgroup of two
+     * chain waves per CU, 93 KB: bq 7.58 against 7.38 ms and c4 8.22 against
+     * 8.05 on one box, profiles/r6_g_ab.txt; reverted.) */
     int ksplit = 0;
     for (int k = 8; k < 32 && !ksplit; k += 8) {
         int nb = 0, nr = 0;
         xmh_stream_create_cus(NULL, 0, k, &nb);
         xmh_stream_create_cus(NULL, k, 32, &nr);
-        if (wgpc * (int64_t)nb >= nwg && nr > 0) ksplit = k;
+        if (2 * (int64_t)nb >= nwg && nr > 0) ksplit = k;
+    }
+    {   /* dev knob XM_FX_KSPLIT=k (8, 16, 24): the biquad's CUs per 32 */
+        const char *e = getenv("XM_FX_KSPLIT");
+        const int kf = e ? atoi(e) : 0;
+        if (kf == 8 || kf == 16 || kf == 24) ksplit = kf;
     }
     if (!ksplit) return XM_ENOSYS;
     const int64_t L = m->table.d.L, M = m->table.d.M;
