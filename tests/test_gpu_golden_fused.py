@@ -50,8 +50,8 @@ _UPS = {(2, 1), (3, 1)}
 
 
 def _fused_mix(L, M, Cc, s16):
-    if s16:   # Q15 mixes: stereo (IO 2) and mono (M16) at the table ratios and the small ones
-        return (L, M) in _TABLE | _SMALL
+    if s16:   # Q15 mixes: stereo (IO 2; 2/1, 3/1, 320/147 since round 6) and mono (M16)
+        return (L, M) != (147, 320) if Cc == 2 else (L, M) in _TABLE | _SMALL
     if Cc == 2:
         return True   # every ratio here: k_rs147_mix (RID), RID_U2, k_rs_d2_mix
     return (L, M) != (147, 320)   # mono f32: 147/320 mono stays generic

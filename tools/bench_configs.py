@@ -558,6 +558,7 @@ def s24to48(a): _shape(a, "s24to48", fi=24000, fo=48000, N=240000, ntr=1)   # st
 def s96to44(a): _shape(a, "s96to44", fi=96000, fo=44100, N=960000, ntr=1)   # stereo 1-track rows at 147/320 (round 5)
 def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)
 def mono1(a): _mono(a, "mono1", 1, 16 * a.mixes, 44100, 48000, 441000)
+def hl(a): _shape(a, "hl")   # the headline's workload through the C API (bench.py's line, here for PMC passes)
 def odd(a): _shape(a, "odd", N=480001)
 def ptrs(a): _shape(a, "ptrs", ptrs=True)
 def far(a): _shape(a, "far", far=True)
@@ -572,6 +573,10 @@ def s16rs2(a): _shape(a, "s16rs2", fmt="s16", ntr=2)
 def s16rs3(a): _shape(a, "s16rs3", fmt="s16", ntr=3)
 def planar2(a): _shape(a, "planar2", planar=True, ntr=2)
 def conv2(a): _shape(a, "conv2", conv=True, ntr=2)
+# stereo s16 Q15 mixes at 2/1, 3/1 and 320/147 (round 6: fused IO kernels; the generic kernel before)
+def s16r24to48(a): _shape(a, "s16r24to48", fi=24000, fo=48000, fmt="s16", N=240000)
+def s16r16to48(a): _shape(a, "s16r16to48", fi=16000, fo=48000, fmt="s16", N=160000)
+def s16r22to48(a): _shape(a, "s16r22to48", fi=22050, fo=48000, fmt="s16", N=220500)
 def stream(a): _shape(a, "stream", stream=True)
 def oconv(a): _shape(a, "oconv", oconv=True)
 

@@ -112,6 +112,11 @@ FUSED_CASES = [
     ("s16_48to44_mono_161", 48000, 44100, 161, 1, 374, "s16"),
     ("s16_48to44_mono_3201", 48000, 44100, 3201, 1, 375, "s16"),
     ("s16_44to48_st_1471", 44100, 48000, 1471, 2, 376, "s16"),
+    # stereo s16 at 2/1, 3/1 and 320/147 (round 6: fused IO kernels)
+    ("s16_24to48_st_1601", 24000, 48000, 1601, 2, 377, "s16"),
+    ("s16_16to48_st_963", 16000, 48000, 963, 2, 378, "s16"),
+    ("s16_22to48_st_1471", 22050, 48000, 1471, 2, 379, "s16"),
+    ("s16_44to96_st_295", 44100, 96000, 295, 2, 380, "s16"),
 ]
 
 
