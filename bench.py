@@ -193,6 +193,20 @@ def traffic_from_profiles():
     return None, f"none on these kernel sources (newest record: {os.path.relpath(files[-1], ROOT)})"
 
 
+def practical_ceiling():
+    """The measured practical HBM ceiling for the headline's byte mix (15.73 GB
+    read + 1.81 GB written): the median over boxes of the best form measured by
+    tools/ubench/hbm_ceiling.hip, committed in profiles/r6_hbm_ceiling.json
+    (tools/dev/ceiling_table.py).  None if the record is absent."""
+    f = os.path.join(ROOT, "profiles", "r6_hbm_ceiling.json")
+    try:
+        with open(f) as fh:
+            d = json.load(fh)
+        return float(d["practical"]["GBps_median"]), os.path.relpath(f, ROOT)
+    except (OSError, ValueError, KeyError, TypeError):
+        return None, None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as fh:
@@ -304,6 +318,7 @@ def headline_line(args, *, n_gpus, shards, B, ntr, N, F, value, ms_per_step, ker
     avg_launch_ms = float(np.mean(kern_ms)) / launches
     achieved = alg_bytes / (avg_launch_ms * 1e-3) / 1e9
     traffic, tsrc = traffic_from_profiles()
+    pgbs, psrc = practical_ceiling()
     cpu = None if args.no_cpu else cpu_baseline(args, ramps)
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "Msamples/s", "n_gpus": n_gpus, "steps": args.steps,
@@ -319,7 +334,11 @@ def headline_line(args, *, n_gpus, shards, B, ntr, N, F, value, ms_per_step, ker
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": tsrc,
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(avg_launch_ms, 4),
-                     "launches_per_step": launches},
+                     "launches_per_step": launches,
+                     "practical": None if pgbs is None else {
+                         "peak": round(pgbs, 1), "unit": "GB/s", "frac": round(achieved / pgbs, 4), "source": psrc,
+                         "what": "best measured form for this byte mix (contiguous mix tiles, nt loads and stores), "
+                                 "median over boxes"}},
         "cpu_baseline": cpu,
     }
     if _BOX:
