@@ -533,7 +533,22 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
      * resample, on the other CUs, fits inside the block being filtered), 6 in
      * the body, 5 and 2 at the tail (the last mix runs after the last filter);
      * 8 blocks ran 0.7 % faster than 10 with a body of 4 (fewer block starts) */
-    static const int cut32[XM_FX_BLOCKS + 1] = {0, 1, 3, 7, 13, 19, 25, 30, 32};
+    int cut[XM_FX_BLOCKS + 1] = {0, 2, 6, 14, 26, 38, 50, 60, 64};   /* 64ths of the clip */
+    {   /* dev knob XM_FX_CUT="c1,...,c7": the inner block starts in 64ths */
+        const char *e = getenv("XM_FX_CUT");
+        int c[XM_FX_BLOCKS + 1] = {0}, n = 1, ok = e != NULL;
+        for (const char *p = e; ok && *p && n < XM_FX_BLOCKS; ++n) {
+            char *end;
+            const long v = strtol(p, &end, 10);
+            ok = end != p && v > c[n - 1] && v < 64;
+            c[n] = (int)v;
+            p = *end == ',' ? end + 1 : end;
+        }
+        if (ok && n == XM_FX_BLOCKS) {
+            c[XM_FX_BLOCKS] = 64;
+            memcpy(cut, c, sizeof cut);
+        }
+    }
     int64_t bs[XM_FX_BLOCKS + 1];
     int K = 0;
     bs[0] = 0;
@@ -545,7 +560,7 @@ static int run_fx_pipelined(XmAudioMixer *m, const XmhMixJob *j0, const XmFxStag
          * mix read whole lines.  Mono rows (1176 x 4 B = 4704 B) start odd
          * blocks 32 B off that grid: correct (stores are range-checked per
          * output), only the line-once property is stereo's */
-        int64_t b = k == XM_FX_BLOCKS ? F : (F * cut32[k] / 32 + 1175) / 1176 * 1176;
+        int64_t b = k == XM_FX_BLOCKS ? F : (F * cut[k] / 64 + 1175) / 1176 * 1176;
         b = b > F ? F : b;
         if (b > bs[K]) bs[++K] = b;
     }
