@@ -5,7 +5,7 @@
  * with -DXM_AB_<NAME> into a copy of the library, to time the kernel's halves
  * apart.  The product build defines none of them, so every
  * constant below is false / its default and each `if constexpr` on them
- * compiles away; every one but XM_AB_PRIO breaks the result.
+ * compiles away; every one but XM_AB_PRIO and XM_AB_DMAPOL breaks the result.
  *   XM_AB_NOWAIT  copy_seg issues no vmcnt wait (the DMA's latency hidden for free)
  *   XM_AB_NODMA   no LDS-DMA instruction (copies read whatever the slot holds)
  *   XM_AB_NOTAPS  no packed taps and no coefficient loads (the memory half alone)
@@ -16,6 +16,9 @@
  *   XM_AB_PPP=n   DMA parts per output pair (a segment's DMA over 8 / n pairs)
  *   XM_AB_ROW0    every coefficient group read from table row 0 (no scalar-cache misses)
  *   XM_AB_PRIO=n  s_setprio 1 for waves 4-7 (n = 1), 0-3 (2) or the odd waves (3)
+ *   XM_AB_DMAPOL=n the input DMA's cache policy for every instantiation: 0 nt, 1 sc1, 2 default
+ *                 (the product: sc1 where segments straddle lines, nt elsewhere; this
+ *                 one keeps the result)
  */
 #ifndef XM_ABLATE_H
 #define XM_ABLATE_H
@@ -70,6 +73,11 @@ constexpr int kPPP = 1;
 constexpr int kPrio = XM_AB_PRIO;
 #else
 constexpr int kPrio = 0;
+#endif
+#ifdef XM_AB_DMAPOL
+constexpr int kDmaPol = XM_AB_DMAPOL;
+#else
+constexpr int kDmaPol = -1;
 #endif
 }  // namespace xm_ab
 
