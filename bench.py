@@ -634,8 +634,8 @@ def box_ids():
     GPU is initialised may not do); skipped under rocprofv3, whose preload
     initialises the GPU first.  Box classes differ in memory-side speed
     (DESIGN §5.3); the line names its box."""
-    if _BOX or any(k.startswith("ROCPROF") for k in os.environ):
-        return _BOX
+    if _BOX or any(k.startswith("ROCPROF") for k in os.environ) or os.environ.get("RANK", "0") != "0":
+        return _BOX   # (rank 0 prints the line)
     import subprocess
     for flag, keys in (("--showmemvendor", ("GPU memory vendor",)), ("--showvbios", ("VBIOS version",)),
                        ("--showserial", ("Serial Number",))):
