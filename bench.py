@@ -156,6 +156,7 @@ def plan(args, world: int, visible: int):
 # the sources the headline kernel is compiled from: a PMC traffic record
 # counts for this run only if it was taken on these very sources
 KERNEL_SOURCES = ("xm-audio-utils_amd/csrc/xm_resample_fast.hip", "xm-audio-utils_amd/csrc/xm_pk_taps.h",
+                  "xm-audio-utils_amd/csrc/xm_ablate.h",
                   "xm-audio-utils_amd/csrc/xm_device.h", "xm-audio-utils_amd/csrc/xm_shim.h",
                   "xm-audio-utils_amd/tools/gen_coefs.c")
 
