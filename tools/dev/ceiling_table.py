@@ -19,6 +19,7 @@ LOGS = {   # box label -> committed ubench log (profiles/), its memory vendor wh
     "C": ("r6_c_hbm_adj.txt", None),
     "D": ("r6_f_hbm_store_forms_samsung.txt", "samsung"),
     "E": ("r6_g_hbm_ceiling.txt", "samsung"),
+    "F": ("r6_z_hbm_ceiling.txt", "samsung"),   # the round-end pass's box (profiles/r6_z_*)
 }
 LINE = re.compile(r"^(.*?)\s+best\s+([\d.]+) ms\s+mean\s+([\d.]+) ms\s+([\d.]+) GB/s")
 
@@ -39,7 +40,7 @@ def main():
         for b, v in rows.get(name, {}).items():
             prod.setdefault(b, v["best_ms"])
     out = {
-        "source": "tools/ubench/hbm_ceiling.hip on five boxes (profiles/r6_*_hbm_*.txt); tools/dev/ceiling_table.py",
+        "source": f"tools/ubench/hbm_ceiling.hip on {len(LOGS)} boxes (profiles/r6_*_hbm_*.txt); tools/dev/ceiling_table.py",
         "bytes": {"read": 15728640000, "write": 1806336000},
         "boxes": vendors,
         "rows": rows,
