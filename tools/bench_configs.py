@@ -556,6 +556,15 @@ def m24to48(a): _mono(a, "m24to48", 1, 16 * a.mixes, 24000, 48000, 240000)   # m
 def m16to48(a): _mono(a, "m16to48", 1, 16 * a.mixes, 16000, 48000, 160000)   # mono 1-track rows at 3/1 (round 5)
 def s24to48(a): _shape(a, "s24to48", fi=24000, fo=48000, N=240000, ntr=1)   # stereo 1-track rows at 2/1 (round 5)
 def s96to44(a): _shape(a, "s96to44", fi=96000, fo=44100, N=960000, ntr=1)   # stereo 1-track rows at 147/320 (round 5)
+def s44to48(a): _shape(a, "s44to48", fi=44100, fo=48000, N=441000, ntr=1)   # stereo 1-track rows at 160/147 (round 6)
+def s32to48(a): _shape(a, "s32to48", fi=32000, fo=48000, N=320000, ntr=1)   # ... at 3/2
+def s48to32(a): _shape(a, "s48to32", fi=48000, fo=32000, N=480000, ntr=1)   # ... at 2/3
+def s96to48(a): _shape(a, "s96to48", fi=96000, fo=48000, N=960000, ntr=1)   # ... at 1/2
+# f32 mixes of 2 and 4 tracks (4 and 2 mixes per wave: split mode's plain stores)
+def t2(a): _shape(a, "t2", ntr=2)
+def t4(a): _shape(a, "t4", ntr=4)
+def t2up(a): _shape(a, "t2up", fi=44100, fo=48000, N=441000, ntr=2)
+def t4up(a): _shape(a, "t4up", fi=44100, fo=48000, N=441000, ntr=4)
 def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)
 def mono1(a): _mono(a, "mono1", 1, 16 * a.mixes, 44100, 48000, 441000)
 def hl(a): _shape(a, "hl")   # the headline's workload through the C API (bench.py's line, here for PMC passes)

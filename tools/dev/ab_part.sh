@@ -13,9 +13,9 @@ OBJ=build/obj_$NAME
 rm -rf $OBJ; mkdir -p $OBJ $NAME
 cp -l build/obj/*.o $OBJ/
 HIPFLAGS="--offload-arch=gfx950 -O3 -fvisibility=hidden -mllvm -pragma-unroll-threshold=100000000 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-rdc -Wall -Wno-unused-result -I../include -Icsrc -Ibuild/gen -fno-slp-vectorize"
-for k in $PARTS; do
-  rm -f $OBJ/xm_resample_fast_p$k.o
-  /opt/rocm/bin/hipcc $HIPFLAGS $DEFS -DXM_FAST_PART=$k -c csrc/xm_resample_fast.hip -o $OBJ/xm_resample_fast_p$k.o
-done
+# the parts in parallel (JOBS at a time, default 4)
+for k in $PARTS; do rm -f $OBJ/xm_resample_fast_p$k.o; done
+printf '%s\n' $PARTS | xargs -P ${JOBS:-4} -I{} /opt/rocm/bin/hipcc $HIPFLAGS $DEFS -DXM_FAST_PART={} \
+  -c csrc/xm_resample_fast.hip -o $OBJ/xm_resample_fast_p{}.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $NAME/libxm_audio.so $OBJ/*.o -lm -ldl -lpthread -Wl,-z,defs -Wl,--no-undefined
 echo "built $NAME/libxm_audio.so ($DEFS, parts $PARTS)"

@@ -19,6 +19,9 @@
  *   XM_AB_DMAPOL=n the input DMA's cache policy for every instantiation: 0 nt, 1 sc1, 2 default
  *                 (the product: sc1 where segments straddle lines, nt elsewhere; this
  *                 one keeps the result)
+ *   XM_AB_DSFAUX=n the cache-policy bits of the DSF / DS grouped mono stores; XM_AB_MONOAUX=n
+ *                 the other mono stores; XM_AB_SPLITAUX=n split mode's whole-segment (SEG) stores;
+ *                 XM_AB_PSPLITAUX=n split mode's plain stores (each keeps the result)
  */
 #ifndef XM_ABLATE_H
 #define XM_ABLATE_H
@@ -78,6 +81,26 @@ constexpr int kPrio = 0;
 constexpr int kDmaPol = XM_AB_DMAPOL;
 #else
 constexpr int kDmaPol = -1;
+#endif
+#ifdef XM_AB_DSFAUX
+constexpr int kDsfAux = XM_AB_DSFAUX;
+#else
+constexpr int kDsfAux = -1;
+#endif
+#ifdef XM_AB_MONOAUX
+constexpr int kMonoAux = XM_AB_MONOAUX;
+#else
+constexpr int kMonoAux = -1;
+#endif
+#ifdef XM_AB_SPLITAUX
+constexpr int kSplitAux = XM_AB_SPLITAUX;
+#else
+constexpr int kSplitAux = -1;
+#endif
+#ifdef XM_AB_PSPLITAUX
+constexpr int kPSplitAux = XM_AB_PSPLITAUX;
+#else
+constexpr int kPSplitAux = -1;
 #endif
 }  // namespace xm_ab
 
