@@ -21,7 +21,8 @@
  *                 one keeps the result)
  *   XM_AB_DSFAUX=n the cache-policy bits of the DSF / DS grouped mono stores; XM_AB_MONOAUX=n
  *                 the other mono stores; XM_AB_SPLITAUX=n split mode's whole-segment (SEG) stores;
- *                 XM_AB_PSPLITAUX=n split mode's plain stores (each keeps the result)
+ *                 XM_AB_PSPLITAUX=n split mode's plain stores; XM_AB_MIXAUX=n the interleaved f32
+ *                 mixes' round stores (each keeps the result)
  */
 #ifndef XM_ABLATE_H
 #define XM_ABLATE_H
@@ -96,6 +97,11 @@ constexpr int kMonoAux = -1;
 constexpr int kSplitAux = XM_AB_SPLITAUX;
 #else
 constexpr int kSplitAux = -1;
+#endif
+#ifdef XM_AB_MIXAUX
+constexpr int kMixAux = XM_AB_MIXAUX;
+#else
+constexpr int kMixAux = -1;
 #endif
 #ifdef XM_AB_PSPLITAUX
 constexpr int kPSplitAux = XM_AB_PSPLITAUX;
