@@ -134,6 +134,8 @@ def plan(args, world: int, visible: int):
             raise SystemExit("bench.py: --devices is for the one-process form, not under torchrun")
         if args.gpus != world:
             raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
+        if world > visible and not rehearsal():
+            raise SystemExit(f"bench.py: {world} ranks but {visible} GPU(s) visible")
         return "ranked", None
     if args.devices:
         devs = [int(d) for d in args.devices.split(",") if d.strip() != ""]
@@ -358,6 +360,16 @@ def mixes_per_shard(args, ntr, shards):
     return args.global_clips // (ntr * shards)
 
 
+def rehearsal() -> bool:
+    """XM_BENCH_REHEARSE=1 (dev only): the torchrun path on a box with fewer
+    GPUs than ranks.  Every rank runs on GPU LOCAL_RANK % visible and the
+    barrier / max-time coordination goes over gloo (RCCL refuses two ranks on
+    one GPU).  Its lines carry "rehearsal": true: they check the multi-rank
+    plumbing (shards, clip ids, barrier, max over ranks, rank 0's line), they
+    are not bench results (the ranks share one GPU)."""
+    return os.environ.get("XM_BENCH_REHEARSE") == "1"
+
+
 def run_headline_ranked(args):
     """One process per GPU (or the plain one-GPU run): rank r, device LOCAL_RANK."""
     import xmaudio as xm
@@ -365,9 +377,15 @@ def run_headline_ranked(args):
 
     rk = xd.from_env()
     world, rank = rk.world, rk.rank
-    torch.cuda.set_device(rk.local)
-    xd.init(rk, "nccl", torch.device("cuda", rk.local))   # RCCL; barrier + max-time only
+    reh = rehearsal() and world > 1
+    local = rk.local % torch.cuda.device_count() if reh else rk.local
+    torch.cuda.set_device(local)
+    if reh:
+        xd.init(rk, "gloo")
+    else:
+        xd.init(rk, "nccl", torch.device("cuda", local))   # RCCL; barrier + max-time only
     dev = torch.cuda.current_device()
+    cdev = "cpu" if reh else "cuda"
 
     ntr, N = args.tracks, args.frames
     B = mixes_per_shard(args, ntr, world)
@@ -407,20 +425,22 @@ def run_headline_ranked(args):
     xd.barrier(rk)
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in zip(ev0, ev1)]
-    elapsed = xd.max_over_ranks(rk, elapsed, device="cuda")
+    elapsed = xd.max_over_ranks(rk, elapsed, device=cdev)
 
     ok = None
     if not args.no_check:   # every rank: its first and last mix vs the oracle
         ok = parity_check(x, y, sorted({0, B - 1}), ramps)
-        ok = xd.min_over_ranks(rk, ok, device="cuda")
+        ok = xd.min_over_ranks(rk, ok, device=cdev)
 
     if rank == 0:
         value = world * B * ntr * N * 2 / (elapsed / args.steps) / 1e6
         par = f"dp{world} (independent mixes, no collective)" + (", one process per GPU" if world > 1 else "")
-        print(json.dumps(headline_line(args, n_gpus=world, shards=world, B=B, ntr=ntr, N=N, F=F, value=value,
-                                       ms_per_step=elapsed / args.steps * 1e3, kern_ms=kern_ms, launches=launches,
-                                       ok=ok, parallelism=par, ramps=ramps,
-                                       mode="torchrun" if world > 1 else "single")), flush=True)
+        line = headline_line(args, n_gpus=world, shards=world, B=B, ntr=ntr, N=N, F=F, value=value,
+                             ms_per_step=elapsed / args.steps * 1e3, kern_ms=kern_ms, launches=launches,
+                             ok=ok, parallelism=par, ramps=ramps, mode="torchrun" if world > 1 else "single")
+        if reh:
+            line["rehearsal"] = True   # the ranks shared one GPU: plumbing check, not a bench result
+        print(json.dumps(line), flush=True)
     xd.finish(rk)
 
 
@@ -571,6 +591,8 @@ def run_c5_ranked(args):
     from xmaudio import dist as xd
 
     rk = xd.from_env()
+    if rehearsal() and rk.world > 1:
+        raise SystemExit("bench.py: XM_BENCH_REHEARSE covers the headline only (config 5's exchange needs RCCL)")
     torch.cuda.set_device(rk.local)
     xd.init(rk, "nccl", torch.device("cuda", rk.local))
     dev = torch.cuda.current_device()

@@ -46,6 +46,16 @@ def test_torchrun_world_must_match():
         _plan(["--gpus", "2", "--devices", "0,1"], world=2)
 
 
+def test_torchrun_ranks_beyond_visible(monkeypatch):
+    """More ranks than GPUs fails loudly, unless the dev rehearsal switch
+    (ranks share one GPU, gloo coordination, lines marked "rehearsal")."""
+    monkeypatch.delenv("XM_BENCH_REHEARSE", raising=False)
+    with pytest.raises(SystemExit):
+        _plan(["--gpus", "2"], world=2, visible=1)
+    monkeypatch.setenv("XM_BENCH_REHEARSE", "1")
+    assert _plan(["--gpus", "2"], world=2, visible=1)[0] == "ranked"
+
+
 def test_config5_ramps_and_shards():
     assert len(bench.RAMPS64) == 64
     args = bench.parse(["--config", "c5"])
