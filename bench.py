@@ -172,12 +172,14 @@ def kernel_src_sha256():
     return h.hexdigest()
 
 
-def traffic_from_profiles():
+def traffic_from_profiles(alg_bytes=None):
     """Corrected PMC traffic per launch (tools/profile_traffic.py output) from
     the newest profiles/*traffic*.json taken on this tree's kernel sources
     (its kernel_src_sha256 equals ours), and the file it came from (a separate
     rocprofv3 pass, not this run).  None when no record matches: a number
-    measured on other kernel code is not reported as this kernel's traffic."""
+    measured on other kernel code is not reported as this kernel's traffic;
+    likewise when the record's launch moved other algorithmic bytes than this
+    one (a shard of the batch at N > 1)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
     if not files:
         return None, None
@@ -192,6 +194,10 @@ def traffic_from_profiles():
         except (OSError, ValueError):
             continue
         if d.get("kernel_src_sha256") == mine:
+            rec = d.get("alg_bytes_per_launch")
+            if alg_bytes is not None and rec is not None and int(rec) != int(alg_bytes):
+                return None, (f"{os.path.relpath(f, ROOT)} holds a launch of {int(rec)} algorithmic bytes "
+                              f"(the 1-GPU batch); this launch moves {int(alg_bytes)}")
             return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
     return None, f"none on these kernel sources (newest record: {os.path.relpath(files[-1], ROOT)})"
 
@@ -320,9 +326,9 @@ def headline_line(args, *, n_gpus, shards, B, ntr, N, F, value, ms_per_step, ker
     alg_bytes = in_samples * 4 + B * F * 2 * 4
     avg_launch_ms = float(np.mean(kern_ms)) / launches
     achieved = alg_bytes / (avg_launch_ms * 1e-3) / 1e9
-    traffic, tsrc = traffic_from_profiles()
+    traffic, tsrc = traffic_from_profiles(alg_bytes)
     pgbs, psrc = practical_ceiling()
-    cpu = None if args.no_cpu else cpu_baseline(args, ramps)
+    cpu = None if args.no_cpu or n_gpus > 1 else cpu_baseline(args, ramps)   # rank 0 at N = 1 only
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "Msamples/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
