@@ -565,6 +565,8 @@ def t2(a): _shape(a, "t2", ntr=2)
 def t4(a): _shape(a, "t4", ntr=4)
 def t2up(a): _shape(a, "t2up", fi=44100, fo=48000, N=441000, ntr=2)
 def t4up(a): _shape(a, "t4up", fi=44100, fo=48000, N=441000, ntr=4)
+def t2odd(a): _shape(a, "t2odd", N=480001, ntr=2)
+def t4odd(a): _shape(a, "t4odd", N=480001, ntr=4)
 def mono8(a): _mono(a, "mono8", 8, 2 * a.mixes, 48000, 44100, 480000)
 def mono1(a): _mono(a, "mono1", 1, 16 * a.mixes, 44100, 48000, 441000)
 def hl(a): _shape(a, "hl")   # the headline's workload through the C API (bench.py's line, here for PMC passes)

@@ -23,6 +23,7 @@
  *                 the other mono stores; XM_AB_SPLITAUX=n split mode's whole-segment (SEG) stores;
  *                 XM_AB_PSPLITAUX=n split mode's plain stores; XM_AB_MIXAUX=n the interleaved f32
  *                 mixes' round stores (each keeps the result)
+ *   XM_AB_SEGALL  the segment stores (SEG) for the 2- and 4-track split layouts too (keeps the result)
  */
 #ifndef XM_ABLATE_H
 #define XM_ABLATE_H
@@ -97,6 +98,11 @@ constexpr int kMonoAux = -1;
 constexpr int kSplitAux = XM_AB_SPLITAUX;
 #else
 constexpr int kSplitAux = -1;
+#endif
+#ifdef XM_AB_SEGALL
+constexpr bool kSegAll = true;
+#else
+constexpr bool kSegAll = false;
 #endif
 #ifdef XM_AB_MIXAUX
 constexpr int kMixAux = XM_AB_MIXAUX;
