@@ -4,6 +4,7 @@ config 2's (--c2: 4096 stereo f32 clips, 48k -> 44.1k), with the output rows
 at strides F + d frames: what does a row base off the 64-B grid cost?  GPU box:
 
     python3 tools/dev/c1_stride.py [--c2] [d ...]      # default d: 0 2 16 32 (c2: 0 1 4 8)
+    python3 tools/dev/c1_stride.py --rows FI FO N B [d ...]   # B stereo f32 1-track rows FI -> FO
 """
 import os
 import sys
@@ -16,9 +17,18 @@ import xmaudio as xm  # noqa: E402
 
 
 def main():
-    c2 = "--c2" in sys.argv[1:]
-    ds = [int(v) for v in sys.argv[1:] if v != "--c2"] or ([0, 1, 4, 8] if c2 else [0, 2, 16, 32])
-    if c2:
+    argv = sys.argv[1:]
+    rows = argv[:1] == ["--rows"]
+    if rows:
+        fi, fo, N, B = (int(v) for v in argv[1:5])
+        argv = argv[5:]
+    c2 = "--c2" in argv or rows
+    ds = [int(v) for v in argv if v != "--c2"] or ([0, 1, 4, 8] if c2 else [0, 2, 16, 32])
+    if rows:
+        C, fmt, esz = 2, "f32", 4
+        m = xm.Mixer(fi, fo, 2, "f32", mem="device")
+        m.set_tracks([dict(gain0=1.0)])
+    elif c2:
         B, N, C, fmt, esz = 4096, 480000, 2, "f32", 4
         m = xm.Mixer(48000, 44100, 2, "f32", mem="device")
     else:
