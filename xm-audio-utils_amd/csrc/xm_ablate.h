@@ -24,6 +24,7 @@
  *                 XM_AB_PSPLITAUX=n split mode's plain stores; XM_AB_MIXAUX=n the interleaved f32
  *                 mixes' round stores (each keeps the result)
  *   XM_AB_SEGALL  the segment stores (SEG) for the 2- and 4-track split layouts too (keeps the result)
+ *   XM_AB_NOMISSEG no segment stores for the 160/147 and 320/147 1-track rows (keeps the result)
  */
 #ifndef XM_ABLATE_H
 #define XM_ABLATE_H
@@ -103,6 +104,11 @@ constexpr int kSplitAux = -1;
 constexpr bool kSegAll = true;
 #else
 constexpr bool kSegAll = false;
+#endif
+#ifdef XM_AB_NOMISSEG
+constexpr bool kNoMisSeg = true;
+#else
+constexpr bool kNoMisSeg = false;
 #endif
 #ifdef XM_AB_MIXAUX
 constexpr int kMixAux = XM_AB_MIXAUX;
