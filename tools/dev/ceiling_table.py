@@ -19,10 +19,11 @@ LOGS = {   # box label -> committed ubench log (profiles/), its memory vendor wh
     "C": ("r6_c_hbm_adj.txt", None),
     "D": ("r6_f_hbm_store_forms_samsung.txt", "samsung"),
     "E": ("r6_g_hbm_ceiling.txt", "samsung"),
-    "F": ("r6_z_hbm_ceiling.txt", "samsung"),   # the round-end passes' boxes (profiles/r6_z_*, r6_z2_*, r6_z3_*, r6_z4_*)
+    "F": ("r6_z_hbm_ceiling.txt", "samsung"),   # the round-end passes' boxes (profiles/r6_z_* ... r6_z5_*)
     "G": ("r6_z2_hbm_ceiling.txt", "samsung"),
     "H": ("r6_z3_hbm_ceiling.txt", "samsung"),
     "I": ("r6_z4_hbm_ceiling.txt", "samsung"),
+    "J": ("r6_z5_hbm_ceiling.txt", "samsung"),
 }
 LINE = re.compile(r"^(.*?)\s+best\s+([\d.]+) ms\s+mean\s+([\d.]+) ms\s+([\d.]+) GB/s")
 
